@@ -1,0 +1,137 @@
+/*
+ * p2p_hip.h -- C ABI of the MI355X (gfx950) Prompt-to-Prompt attention-control library.
+ *
+ * Every entry point replaces one call site of the reference's attention-control hot path
+ * (KIMGEONUNG/prompt-to-prompt; file:line below).  Conventions:
+ *   - all tensor pointers are DEVICE pointers, row-major, caller-owned; the library never
+ *     allocates, never synchronises, and launches on the given stream only;
+ *   - small per-call tables (batch index maps, group lists) are HOST arrays, copied into the
+ *     kernel arguments (no device upload per call);
+ *   - the return value is 0 on success, a hipError_t value (> 0) on a launch failure, or a
+ *     negative P2P_E_* code when the arguments are rejected before anything is launched.
+ *   - q/k/v/o use the projection layout [n_batch, tokens, n_heads * head_dim] (the to_q /
+ *     to_k / to_v outputs); the head split of ptp_utils.py:191-193 and the merge of :207 are
+ *     done by strides, not copies.
+ */
+#ifndef P2P_HIP_H
+#define P2P_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P2P_ABI_VERSION 1
+#define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
+#define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
+#define P2P_MAX_KEYS_CROSS 96
+#define P2P_PROGRAM_COLS 128 /* column stride of an edit program (>= n_key + 1)      */
+
+enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };
+enum { P2P_COMPUTE_BF16 = 0, P2P_COMPUTE_F32 = 1 };
+
+enum {
+  P2P_E_ARG = -1,       /* null pointer / inconsistent sizes                             */
+  P2P_E_HEAD_DIM = -2,  /* head_dim without a compiled kernel                             */
+  P2P_E_DTYPE = -3,     /* io_dtype / compute combination not supported                   */
+  P2P_E_KEYS = -4,      /* n_key above P2P_MAX_KEYS_CROSS for the cross kernel            */
+  P2P_E_BATCH = -5,     /* n_batch above P2P_MAX_BATCH or group list inconsistent         */
+  P2P_E_ALIGN = -6      /* a pointer / stride breaks the 16-byte vector-load alignment    */
+};
+
+typedef void* p2p_stream_t; /* a hipStream_t */
+
+/* One attention call: q [n_batch, n_query, *], k/v [n_batch, n_key, *], o like q.
+ * Strides are in elements.  scale is CrossAttention.scale (head_dim ** -0.5,
+ * ptp_utils.py:195). */
+typedef struct {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  int64_t q_row_stride, k_row_stride, v_row_stride, o_row_stride;
+  int64_t q_batch_stride, k_batch_stride, v_batch_stride, o_batch_stride;
+  int32_t n_batch, n_query, n_key, n_heads, head_dim;
+  int32_t io_dtype; /* P2P_DTYPE_*  (element type of q, k, v, o)                      */
+  int32_t compute;  /* P2P_COMPUTE_* (bf16 MFMA, or exact-f32 MFMA check mode)          */
+  float scale;
+} p2p_attn_tensors;
+
+/* Self-attention (ptp_utils.py:183-208 with context=None) fused with the controller's
+ * self-attention edit and the AttentionStore epilogue:
+ *   O[n] = softmax(Q[qk_src[n]] K[qk_src[n]]^T * scale) V[n]
+ * qk_src (host, n_batch entries, NULL = identity) implements the source-map injection of
+ * AttentionControlEdit.replace_self_attention (main.py:169-174, null_text.py:224-230): an
+ * edit inside the self_replace window reads the SOURCE prompt's probabilities and its OWN
+ * values.  store (nullable) receives the normalised probabilities of every entry whose
+ * store_slot (host) is >= 0 at maps [store_slot[n] + head] of a [*, n_query, n_key] f32
+ * tensor, overwritten (store_accumulate = 0, first step) or added (= 1): the running sum
+ * of AttentionStore.between_steps (main.py:135-142). */
+int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store,
+                      const int32_t* store_slot, int32_t store_accumulate, p2p_stream_t stream);
+
+/* A prompt group of a cross-attention launch: entries [first, first + count) of the batch;
+ * entry `first` is the source prompt, the others its edits (main.py:187).  program is the
+ * device edit program (layout: P2P_PROGRAM_COLS-strided tables) or NULL
+ * for no edit; alpha is the device [count - 1][n_key] row cross_replace_alpha[cur_step]
+ * (main.py:189). */
+typedef struct {
+  int32_t first;
+  int32_t count;
+  const void* program;
+  const float* alpha;
+} p2p_group;
+
+/* Cross-attention (ptp_utils.py:183-208 with context=...) with the controller's cross edit
+ * applied in registers between softmax and PV (AttentionControlEdit.forward, main.py:180-197:
+ * Replace :217-218, Refine :235-239, Reweight :258-264) and the AttentionStore epilogue
+ * (store/store_slot/store_accumulate as for p2p_self_attn_fwd; stored maps are the
+ * post-edit probabilities, as the reference's aliasing store holds). */
+int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32_t n_groups,
+                       float* store, const int32_t* store_slot, int32_t store_accumulate,
+                       p2p_stream_t stream);
+
+/* Materialise mode, for controllers that override forward(attn, ...) (the reference
+ * protocol, main.py:85-98): probs[n*H + h] = softmax(Q K^T * scale) as an f32
+ * [n_batch * n_heads, n_query, n_key] tensor (ptp_utils.py:195-204).  key_mask (nullable,
+ * uint8 [n_batch, n_key], nonzero = keep) reproduces ptp_utils.py:197-201, including its
+ * head-major repeat of the mask rows. */
+int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* probs,
+                   p2p_stream_t stream);
+
+/* Materialise mode, second half: O[n] = probs[n*H + h] V[n] (ptp_utils.py:206-207). */
+int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stream);
+
+/* LocalBlend (null_text.py:41-70; main.py:35-52 is the B=2 special case) for one prompt
+ * group: maps[l] are the running-sum cross maps of the five 16x16 layers
+ * (down_cross[2:4] + up_cross[:3]), each [n_prompts * heads_per_map, 256, n_words] f32. */
+typedef struct {
+  const float* maps[8];
+  int32_t n_maps;
+  int32_t heads_per_map;
+  int32_t n_prompts;
+  int32_t n_words;
+  int32_t map_res;                 /* 16                                               */
+  const float* alpha_layers;       /* [n_prompts, n_words]                             */
+  const float* substruct_layers;   /* [n_prompts, n_words] or NULL                     */
+  float th_pool, th_sub;           /* th[0], th[1] (main form: threshold, unused)      */
+  float* x_t;                      /* [n_prompts, channels, lat_h, lat_w] in/out       */
+  int32_t channels, lat_h, lat_w;
+  float* word_sums;                /* workspace [n_prompts, 2, n_maps*heads, res*res]  */
+  uint8_t* mask_out;               /* optional [n_prompts, lat_h, lat_w] final mask    */
+} p2p_blend_args;
+
+int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream);
+
+/* AttentionStore.get_average_attention (main.py:144-149): dst = src / divisor. */
+int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream);
+
+/* Build/runtime information. */
+int p2p_abi_version(void);
+const char* p2p_error_string(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P2P_HIP_H */

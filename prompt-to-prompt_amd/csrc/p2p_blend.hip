@@ -1,0 +1,169 @@
+// LocalBlend and AttentionStore helpers (bandwidth-bound, no MFMA).
+//
+// LocalBlend (null_text.py:41-70; main.py:35-52 is the two-prompt case):
+//   maps   = cat_l reshape(store_l, [B, H, 1, 16, 16, W])           -> [B, L*H, 1, 16, 16, W]
+//   m      = (maps * alpha).sum(-1).mean(1)                           -> [B, 1, 16, 16]
+//   m      = max_pool2d(m, 3, 1, 1)          (pooled mask only)
+//   m      = interpolate(m, x_t.shape[2:])   (nearest)
+//   mask   = (m / max_{y,x} m) > th;  mask = mask[:1] | mask
+//   mask  &= ~(substruct mask)               (optional, unpooled, th[1])
+//   x_t    = x_t[:1] + mask * (x_t - x_t[:1])
+// Kernel 1 reduces the word axis for every (prompt, layer x head) map; kernel 2 does the rest
+// for the whole prompt group in one workgroup (the mask of prompt 0 gates every other prompt).
+#include "p2p_device.h"
+#include "p2p_kernels.h"
+
+namespace p2p {
+
+constexpr int kBlendMaxPrompts = 16;
+
+// grid (n_prompts, n_maps * heads), block = res*res threads (one per pixel)
+__global__ __launch_bounds__(256) void blend_wordsum_kernel(p2p_blend_args a) {
+  const int b = blockIdx.x;
+  const int j = blockIdx.y;                 // l * heads + hd
+  const int l = j / a.heads_per_map;
+  const int hd = j - l * a.heads_per_map;
+  const int R2 = a.map_res * a.map_res;
+  const int W = a.n_words;
+  __shared__ float sa[128], ss[128];
+  for (int w = threadIdx.x; w < W; w += blockDim.x) {
+    sa[w] = a.alpha_layers[b * W + w];
+    ss[w] = a.substruct_layers ? a.substruct_layers[b * W + w] : 0.f;
+  }
+  __syncthreads();
+  const int pix = threadIdx.x;
+  if (pix >= R2) return;
+  const float* m = a.maps[l] + ((int64_t)(b * a.heads_per_map + hd) * R2 + pix) * W;
+  float acc_a = 0.f, acc_s = 0.f;
+  for (int w = 0; w < W; ++w) {
+    const float v = m[w];
+    acc_a += v * sa[w];
+    acc_s += v * ss[w];
+  }
+  const int LH = a.n_maps * a.heads_per_map;
+  a.word_sums[((int64_t)(b * 2 + 0) * LH + j) * R2 + pix] = acc_a;
+  a.word_sums[((int64_t)(b * 2 + 1) * LH + j) * R2 + pix] = acc_s;
+}
+
+// x0 + m * (xb - x0) rounded exactly as the reference's three tensor ops (no fma contraction)
+__device__ __forceinline__ float blend1(float x0, float xb, float m) {
+#pragma clang fp contract(off)
+  const float diff = xb - x0;
+  const float t = m * diff;
+  return x0 + t;
+}
+
+// one workgroup for the whole prompt group
+__global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
+  const int B = a.n_prompts;
+  const int R = a.map_res;
+  const int R2 = R * R;
+  const int LH = a.n_maps * a.heads_per_map;
+  const int HW = a.lat_h * a.lat_w;
+  __shared__ float mean_a[kBlendMaxPrompts][256];
+  __shared__ float mean_s[kBlendMaxPrompts][256];
+  __shared__ float pooled[kBlendMaxPrompts][256];
+  __shared__ float vmax[kBlendMaxPrompts][2];
+  const int tid = threadIdx.x;
+  const bool sub = a.substruct_layers != nullptr;
+
+  // mean over the L*H maps (sum in index order, then / L*H as Tensor.mean does)
+  for (int i = tid; i < B * R2; i += blockDim.x) {
+    const int b = i / R2, pix = i - b * R2;
+    float sa = 0.f, ss = 0.f;
+    for (int j = 0; j < LH; ++j) {
+      sa += a.word_sums[((int64_t)(b * 2 + 0) * LH + j) * R2 + pix];
+      ss += a.word_sums[((int64_t)(b * 2 + 1) * LH + j) * R2 + pix];
+    }
+    mean_a[b][pix] = sa / (float)LH;
+    mean_s[b][pix] = ss / (float)LH;
+  }
+  __syncthreads();
+  // 3x3 max-pool, stride 1, padding 1 (padding never wins: -inf)
+  for (int i = tid; i < B * R2; i += blockDim.x) {
+    const int b = i / R2, pix = i - b * R2;
+    const int y = pix / R, x = pix - y * R;
+    float m = -INFINITY;
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int yy = y + dy, xx = x + dx;
+        if (yy >= 0 && yy < R && xx >= 0 && xx < R) m = fmaxf(m, mean_a[b][yy * R + xx]);
+      }
+    pooled[b][pix] = m;
+  }
+  __syncthreads();
+  // per-image max of the nearest-upsampled maps = max over the sampled source pixels
+  const float sy = (float)R / (float)a.lat_h, sx = (float)R / (float)a.lat_w;
+  if (tid < 2 * B) {
+    const int b = tid >> 1, which = tid & 1;
+    float m = -INFINITY;
+    for (int Y = 0; Y < a.lat_h; ++Y) {
+      const int y = min((int)floorf(Y * sy), R - 1);
+      for (int X = 0; X < a.lat_w; ++X) {
+        const int x = min((int)floorf(X * sx), R - 1);
+        m = fmaxf(m, which == 0 ? pooled[b][y * R + x] : mean_s[b][y * R + x]);
+      }
+    }
+    vmax[b][which] = m;
+  }
+  __syncthreads();
+  // masks + latent blend: x_t[b] = x_t[0] + mask * (x_t[b] - x_t[0])
+  for (int i = tid; i < B * HW; i += blockDim.x) {
+    const int b = i / HW, yx = i - b * HW;
+    const int Y = yx / a.lat_w, X = yx - Y * a.lat_w;
+    const int src = min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
+    bool m0 = pooled[0][src] / vmax[0][0] > a.th_pool;
+    bool mb = pooled[b][src] / vmax[b][0] > a.th_pool;
+    bool mask = m0 || mb;
+    if (sub) {
+      const bool s0 = mean_s[0][src] / vmax[0][1] > a.th_sub;
+      const bool sb = mean_s[b][src] / vmax[b][1] > a.th_sub;
+      mask = mask && !(s0 || sb);
+    }
+    const float mf = mask ? 1.f : 0.f;
+    if (a.mask_out) a.mask_out[(int64_t)b * HW + yx] = mask ? 1 : 0;
+    if (b == 0) continue;  // x_t[0] + mask * 0 == x_t[0]
+    for (int ch = 0; ch < a.channels; ++ch) {
+      const float x0 = a.x_t[(int64_t)(0 * a.channels + ch) * HW + yx];
+      float* xb = a.x_t + (int64_t)(b * a.channels + ch) * HW + yx;
+      *xb = blend1(x0, *xb, mf);
+    }
+  }
+}
+
+__global__ void store_scale_kernel(const float* __restrict__ src, float* __restrict__ dst, float divisor,
+                                   int64_t n) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4_t v = reinterpret_cast<const f32x4_t*>(src)[i];
+    v[0] = v[0] / divisor; v[1] = v[1] / divisor; v[2] = v[2] / divisor; v[3] = v[3] / divisor;
+    reinterpret_cast<f32x4_t*>(dst)[i] = v;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = src[i] / divisor;
+}
+
+int run_localblend(const p2p_blend_args& a, hipStream_t st) {
+  if (a.n_prompts < 1 || a.n_prompts > kBlendMaxPrompts || a.map_res * a.map_res > 256 || a.n_words > 128 ||
+      a.n_maps < 1 || a.n_maps > 8 || !a.alpha_layers || !a.x_t || !a.word_sums)
+    return P2P_E_ARG;
+  for (int l = 0; l < a.n_maps; ++l)
+    if (!a.maps[l]) return P2P_E_ARG;
+  dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map);
+  hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(blend_finalize_kernel, dim3(1), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)src | (uintptr_t)dst) & 15) return P2P_E_ALIGN;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(store_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, divisor, n);
+  return (int)hipGetLastError();
+}
+
+}  // namespace p2p

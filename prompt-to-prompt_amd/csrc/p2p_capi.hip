@@ -1,0 +1,157 @@
+// extern "C" entry points of libp2p_hip.so (declared in include/p2p_hip.h).
+// Validation happens here, before anything is launched: a rejected call returns a negative
+// P2P_E_* code and touches nothing.
+#include "p2p_kernels.h"
+
+using namespace p2p;
+
+namespace {
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int check_tensors(const p2p_attn_tensors* t, bool need_q, bool need_k, bool need_v, bool need_o) {
+  if (!t) return P2P_E_ARG;
+  if ((need_q && !t->q) || (need_k && !t->k) || (need_v && !t->v) || (need_o && !t->o)) return P2P_E_ARG;
+  if (t->n_batch < 1 || t->n_query < 1 || t->n_key < 1 || t->n_heads < 1 || t->head_dim < 8) return P2P_E_ARG;
+  if (t->n_batch > P2P_MAX_BATCH) return P2P_E_BATCH;
+  if (t->head_dim % 8) return P2P_E_HEAD_DIM;
+  if (t->io_dtype != P2P_DTYPE_F32 && t->io_dtype != P2P_DTYPE_BF16) return P2P_E_DTYPE;
+  if (t->compute != P2P_COMPUTE_BF16 && t->compute != P2P_COMPUTE_F32) return P2P_E_DTYPE;
+  const int es = t->io_dtype == P2P_DTYPE_F32 ? 4 : 2;
+  // 16-byte vector loads of 8-element chunks need every row/head offset 8-element aligned
+  const int64_t strides[8] = {t->q_row_stride, t->k_row_stride, t->v_row_stride, t->o_row_stride,
+                              t->q_batch_stride, t->k_batch_stride, t->v_batch_stride, t->o_batch_stride};
+  for (int i = 0; i < 8; ++i)
+    if ((strides[i] * es) % 16) return P2P_E_ALIGN;
+  if ((need_q && !aligned16(t->q)) || (need_k && !aligned16(t->k)) || (need_v && !aligned16(t->v)) ||
+      (need_o && !aligned16(t->o)))
+    return P2P_E_ALIGN;
+  return 0;
+}
+
+template <typename A>
+void fill_common(A& a, const p2p_attn_tensors* t) {
+  a.q = t->q; a.k = t->k; a.v = t->v; a.o = t->o;
+  a.ldq = t->q_row_stride; a.ldk = t->k_row_stride; a.ldv = t->v_row_stride; a.ldo = t->o_row_stride;
+  a.bsq = t->q_batch_stride; a.bsk = t->k_batch_stride; a.bsv = t->v_batch_stride; a.bso = t->o_batch_stride;
+  a.N = t->n_batch; a.P = t->n_query; a.K = t->n_key; a.H = t->n_heads;
+  a.scale_log2 = t->scale * 1.4426950408889634f;
+  a.n_qtiles = 0;
+  a.store = nullptr;
+  a.store_accumulate = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2p_abi_version(void) { return P2P_ABI_VERSION; }
+
+const char* p2p_error_string(int code) {
+  switch (code) {
+    case 0: return "ok";
+    case P2P_E_ARG: return "invalid argument";
+    case P2P_E_HEAD_DIM: return "head_dim has no compiled kernel";
+    case P2P_E_DTYPE: return "unsupported io_dtype/compute combination";
+    case P2P_E_KEYS: return "n_key above P2P_MAX_KEYS_CROSS";
+    case P2P_E_BATCH: return "batch / group list out of range";
+    case P2P_E_ALIGN: return "pointer or stride breaks 16-byte alignment";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+  }
+}
+
+int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store, const int32_t* store_slot,
+                      int32_t store_accumulate, p2p_stream_t stream) {
+  int rc = check_tensors(t, true, true, true, true);
+  if (rc) return rc;
+  SelfArgs a;
+  fill_common(a, t);
+  a.probs = nullptr;
+  a.key_mask = nullptr;
+  bool any_store = false;
+  for (int n = 0; n < t->n_batch; ++n) {
+    a.qk_src[n] = qk_src ? qk_src[n] : n;
+    if (a.qk_src[n] < 0 || a.qk_src[n] >= t->n_batch) return P2P_E_BATCH;
+    a.store_slot[n] = (store && store_slot) ? store_slot[n] : -1;
+    any_store |= a.store_slot[n] >= 0;
+  }
+  if (any_store && !aligned16(store)) return P2P_E_ALIGN;
+  a.store = any_store ? store : nullptr;
+  a.store_accumulate = store_accumulate ? 1 : 0;
+  return run_self(a, t->io_dtype, t->compute, t->head_dim, any_store ? MODE_STORE_ : MODE_FUSED_,
+                  (hipStream_t)stream);
+}
+
+int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32_t n_groups, float* store,
+                       const int32_t* store_slot, int32_t store_accumulate, p2p_stream_t stream) {
+  int rc = check_tensors(t, true, true, true, true);
+  if (rc) return rc;
+  if (t->n_key > P2P_MAX_KEYS_CROSS) return P2P_E_KEYS;
+  if (!groups || n_groups < 1 || n_groups > P2P_MAX_GROUPS) return P2P_E_BATCH;
+  CrossArgs a;
+  fill_common(a, t);
+  int covered = 0;
+  for (int g = 0; g < n_groups; ++g) {
+    const p2p_group& G = groups[g];
+    if (G.first < 0 || G.count < 1 || G.first + G.count > t->n_batch) return P2P_E_BATCH;
+    if (G.program && G.count > 1 && !G.alpha) return P2P_E_ARG;
+    a.grp_first[g] = G.first;
+    a.grp_count[g] = G.count;
+    a.grp_prog[g] = G.program;
+    a.grp_alpha[g] = G.alpha;
+    covered += G.count;
+  }
+  if (covered != t->n_batch) return P2P_E_BATCH;
+  bool any_store = false;
+  for (int n = 0; n < t->n_batch; ++n) {
+    a.store_slot[n] = (store && store_slot) ? store_slot[n] : -1;
+    any_store |= a.store_slot[n] >= 0;
+  }
+  a.store = any_store ? store : nullptr;
+  a.store_accumulate = store_accumulate ? 1 : 0;
+  return run_cross(a, t->io_dtype, t->compute, t->head_dim, n_groups, (hipStream_t)stream);
+}
+
+int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* probs, p2p_stream_t stream) {
+  int rc = check_tensors(t, true, true, false, false);
+  if (rc) return rc;
+  if (!probs) return P2P_E_ARG;
+  SelfArgs a;
+  fill_common(a, t);
+  a.probs = nullptr;
+  a.key_mask = key_mask;
+  a.store = probs;
+  a.store_accumulate = 0;
+  for (int n = 0; n < t->n_batch; ++n) {
+    a.qk_src[n] = n;
+    a.store_slot[n] = n * t->n_heads;
+  }
+  return run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_PROBS_, (hipStream_t)stream);
+}
+
+int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stream) {
+  int rc = check_tensors(t, false, false, true, true);
+  if (rc) return rc;
+  if (!probs) return P2P_E_ARG;
+  SelfArgs a;
+  fill_common(a, t);
+  a.probs = probs;
+  a.key_mask = nullptr;
+  for (int n = 0; n < t->n_batch; ++n) {
+    a.qk_src[n] = n;
+    a.store_slot[n] = -1;
+  }
+  return run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_PV_, (hipStream_t)stream);
+}
+
+int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream) {
+  if (!a) return P2P_E_ARG;
+  return run_localblend(*a, (hipStream_t)stream);
+}
+
+int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream) {
+  if (!src || !dst) return P2P_E_ARG;
+  return run_store_scale(src, dst, divisor, n, (hipStream_t)stream);
+}
+
+}  // extern "C"

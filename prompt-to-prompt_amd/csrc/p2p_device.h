@@ -1,0 +1,261 @@
+// Device-side building blocks for the Prompt-to-Prompt attention kernels (gfx950 / CDNA4).
+//
+// Fragment convention used by every kernel in this library:
+//   * scores are computed TRANSPOSED, S^T = K * Q^T, with v_mfma_f32_32x32x16_bf16 (or the
+//     exact-f32 v_mfma_f32_32x32x2_f32 in check mode).  A 32x32 S^T block leaves the query q on
+//     the lane (q = lane & 31) and 16 keys in the 16 accumulator registers:
+//         key(r, h) = (r & 3) + 8 * (r >> 2) + 4 * h,   h = lane >> 5.
+//     A softmax row (one query) therefore lives in ONE lane pair (q, q+32): row max / row sum
+//     are 16 register ops plus one cross-half exchange.
+//   * the PV product is computed transposed too, O^T = V^T * P^T, with the S^T accumulator
+//     used directly as the B operand (no LDS round trip for P).  O^T leaves q on the lane, so
+//     the online-softmax rescale and the final 1/l are per-lane scalars.
+//   * an "8-element k fragment" is the same data in both precisions: lane (row = lane&31,
+//     h = lane>>5) holds elements k = 8h + j, j = 0..7.  bf16 packs them into one MFMA; f32
+//     issues 8 MFMAs (k pair {j, 8+j} each), which sums the same 16 products.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2p {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(8))) short short8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ uint16_t f2bf(float x) {
+  return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+__device__ __forceinline__ float bf2f(uint16_t x) {
+  return __builtin_bit_cast(float, ((uint32_t)x) << 16);
+}
+
+// S^T / O^T accumulator row for register r of lane-half h.
+__device__ __forceinline__ constexpr int acc_row(int r, int h) {
+  return (r & 3) + 8 * (r >> 2) + 4 * h;
+}
+
+// ------------------------------------------------------------------ precision traits
+// bf16 operands, f32 accumulate: the production path.
+struct MmaBf16 {
+  using elem = uint16_t;  // LDS / operand element
+  struct frag {
+    short8_t v;
+  };
+  static constexpr int kElemBytes = 2;
+
+  __device__ __forceinline__ static void mma(f32x16_t& acc, const frag& a, const frag& b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a.v),
+                                                  __builtin_bit_cast(bf16x8_t, b.v), acc, 0, 0, 0);
+  }
+  __device__ __forceinline__ static elem from_float(float x) { return f2bf(x); }
+  // 8 consecutive elements from LDS (16-byte aligned).
+  __device__ __forceinline__ static frag load8(const elem* p) {
+    frag f;
+    f.v = *reinterpret_cast<const short8_t*>(p);
+    return f;
+  }
+  __device__ __forceinline__ static frag zero() {
+    frag f;
+    f.v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    return f;
+  }
+  // Pack accumulator registers [8s, 8s+8) of an S^T block into a B fragment.
+  __device__ __forceinline__ static frag pack_p(const float* p) {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = (short)f2bf(p[j]);
+    return f;
+  }
+};
+
+// Exact f32 operands (v_mfma_f32_32x32x2_f32): the 1e-5 check mode.
+struct MmaF32 {
+  using elem = float;
+  struct frag {
+    float v[8];
+  };
+  static constexpr int kElemBytes = 4;
+
+  __device__ __forceinline__ static void mma(f32x16_t& acc, const frag& a, const frag& b) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.v[j], b.v[j], acc, 0, 0, 0);
+  }
+  __device__ __forceinline__ static elem from_float(float x) { return x; }
+  __device__ __forceinline__ static frag load8(const elem* p) {
+    frag f;
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p);
+    const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + 4);
+    f.v[0] = a[0]; f.v[1] = a[1]; f.v[2] = a[2]; f.v[3] = a[3];
+    f.v[4] = b[0]; f.v[5] = b[1]; f.v[6] = b[2]; f.v[7] = b[3];
+    return f;
+  }
+  __device__ __forceinline__ static frag zero() {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = 0.f;
+    return f;
+  }
+  __device__ __forceinline__ static frag pack_p(const float* p) {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = p[j];
+    return f;
+  }
+};
+
+// ------------------------------------------------------------------ global I/O helpers
+// Load 8 consecutive input elements (fp32 or bf16 in HBM) and convert to the MMA element.
+template <typename IO, typename M>
+__device__ __forceinline__ void load8_global(const IO* src, typename M::elem* dst8);
+
+template <>
+__device__ __forceinline__ void load8_global<float, MmaBf16>(const float* src, uint16_t* dst8) {
+  const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+  const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
+  dst8[0] = f2bf(a[0]); dst8[1] = f2bf(a[1]); dst8[2] = f2bf(a[2]); dst8[3] = f2bf(a[3]);
+  dst8[4] = f2bf(b[0]); dst8[5] = f2bf(b[1]); dst8[6] = f2bf(b[2]); dst8[7] = f2bf(b[3]);
+}
+template <>
+__device__ __forceinline__ void load8_global<uint16_t, MmaBf16>(const uint16_t* src, uint16_t* dst8) {
+  *reinterpret_cast<short8_t*>(dst8) = *reinterpret_cast<const short8_t*>(src);
+}
+template <>
+__device__ __forceinline__ void load8_global<float, MmaF32>(const float* src, float* dst8) {
+  *reinterpret_cast<f32x4_t*>(dst8) = *reinterpret_cast<const f32x4_t*>(src);
+  *reinterpret_cast<f32x4_t*>(dst8 + 4) = *reinterpret_cast<const f32x4_t*>(src + 4);
+}
+
+// Raw register staging: the global bytes of one 8-element chunk, converted at LDS-write time.
+template <typename IO>
+struct Chunk8;
+template <>
+struct Chunk8<float> {
+  f32x4_t a, b;
+  __device__ __forceinline__ void load(const float* src) {
+    a = *reinterpret_cast<const f32x4_t*>(src);
+    b = *reinterpret_cast<const f32x4_t*>(src + 4);
+  }
+  __device__ __forceinline__ void clear() {
+    a = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    b = a;
+  }
+  __device__ __forceinline__ void store(uint16_t* dst) const {
+    short8_t v;
+    v[0] = (short)f2bf(a[0]); v[1] = (short)f2bf(a[1]); v[2] = (short)f2bf(a[2]); v[3] = (short)f2bf(a[3]);
+    v[4] = (short)f2bf(b[0]); v[5] = (short)f2bf(b[1]); v[6] = (short)f2bf(b[2]); v[7] = (short)f2bf(b[3]);
+    *reinterpret_cast<short8_t*>(dst) = v;
+  }
+  __device__ __forceinline__ void store(float* dst) const {
+    *reinterpret_cast<f32x4_t*>(dst) = a;
+    *reinterpret_cast<f32x4_t*>(dst + 4) = b;
+  }
+};
+template <>
+struct Chunk8<uint16_t> {
+  short8_t v;
+  __device__ __forceinline__ void load(const uint16_t* src) { v = *reinterpret_cast<const short8_t*>(src); }
+  __device__ __forceinline__ void clear() { v = short8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+  __device__ __forceinline__ void store(uint16_t* dst) const { *reinterpret_cast<short8_t*>(dst) = v; }
+  __device__ __forceinline__ void store(float* dst) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j] = bf2f((uint16_t)v[j]);
+  }
+};
+
+// Store 4 consecutive f32 results as IO elements.
+__device__ __forceinline__ void store4(float* dst, float a, float b, float c, float d) {
+  *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{a, b, c, d};
+}
+__device__ __forceinline__ void store4(uint16_t* dst, float a, float b, float c, float d) {
+  short4_t v;
+  v[0] = (short)f2bf(a); v[1] = (short)f2bf(b); v[2] = (short)f2bf(c); v[3] = (short)f2bf(d);
+  *reinterpret_cast<short4_t*>(dst) = v;
+}
+
+// ------------------------------------------------------------------ V^T operand fragments
+// A operand of the PV MFMA for k-step s (16 keys) of a 32-key sub-block starting at LDS row
+// `row0`, output columns [col0, col0+32): lane (d = lane&31, h) needs
+//   V[row0 + 16s + 8(j>>2) + 4h + (j&3)][col0 + d],  j = 0..7
+// which two ds_read_b64_tr_b16 deliver from a row-major [keys][VS] bf16 image.
+template <int VS>
+__device__ __forceinline__ MmaBf16::frag vt_frag(const uint16_t* V, int row0, int s, int col0, int lane) {
+  const int h = lane >> 5;
+  const int r = row0 + 16 * s + 4 * h + ((lane & 15) >> 2);
+  const int c = col0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  typedef __attribute__((address_space(3))) short4_t lds_s4;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(V + r * VS + c));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(V + (r + 8) * VS + c));
+  MmaBf16::frag f;
+  f.v = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return f;
+}
+
+// PV for one 32-key sub-block with the transposed-accumulator convention, bf16 path:
+// O[dt] += V^T[dt*32.., sub-block keys] * P^T[sub-block keys, q].
+template <int VS, int NDT>
+__device__ __forceinline__ void pv_block(MmaBf16, f32x16_t (&O)[NDT], const uint16_t* V, int row0,
+                                         const float (&p)[16], int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const MmaBf16::frag b = MmaBf16::pack_p(p + 8 * s);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const MmaBf16::frag a = vt_frag<VS>(V, row0, s, dt * 32, lane);
+      MmaBf16::mma(O[dt], a, b);
+    }
+  }
+}
+
+// Exact-f32 path: 16 MFMAs (32x32x2) per sub-block and d-tile; MFMA t takes keys
+// acc_row(t, h) from lane half h, which is exactly accumulator register t of the S^T block.
+template <int VS, int NDT>
+__device__ __forceinline__ void pv_block(MmaF32, f32x16_t (&O)[NDT], const float* V, int row0,
+                                         const float (&p)[16], int lane) {
+  const int h = lane >> 5;
+  const int d = lane & 31;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const float* vr = V + (row0 + acc_row(t, h)) * VS + d;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+      O[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[dt * 32], p[t], O[dt], 0, 0, 0);
+  }
+}
+
+// ------------------------------------------------------------------ XCD-aware block remap
+// Consecutive logical ids land on the same XCD (blocks b and b+8 share one under the
+// observed round-robin dispatch); bijective for any grid size.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Row stride (in elements) of an LDS tile read with ds_read_b128 by 16 distinct rows at the
+// same column: a byte stride of 16 * odd spreads any 16 consecutive rows over all 16 slots.
+template <int D, int ES>
+struct KStride {
+  static constexpr int bytes0 = D * ES;
+  static constexpr int bytes = ((bytes0 / 16) % 2 == 0) ? bytes0 + 16 : bytes0;
+  static constexpr int value = bytes / ES;
+};
+
+// Row stride (elements) of the bf16 V image read with ds_read_b64_tr_b16: the 4 rows x 2
+// column groups one 32-lane half reads must fall on 8 distinct 8-dword bank slots, i.e.
+// stride (dwords) = 16 or 48 mod 64.
+template <int DV>
+struct VStrideBf16 {
+  static constexpr int dw0 = DV / 2;
+  static constexpr int value = ((dw0 % 64) == 16 || (dw0 % 64) == 48) ? DV : (dw0 < 48 ? 96 : (dw0 < 80 ? 160 : 224));
+};
+
+}  // namespace p2p

@@ -1,0 +1,55 @@
+// Kernel-argument structs shared by the kernels and the C-ABI shim (passed by value).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/p2p_hip.h"
+
+namespace p2p {
+
+struct SelfArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  int64_t ldq, ldk, ldv, ldo;  // token strides (elements)
+  int64_t bsq, bsk, bsv, bso;  // batch strides (elements)
+  int N, P, K, H;
+  float scale_log2;            // CrossAttention.scale * log2(e)
+  int n_qtiles;
+  float* store;                // AttentionStore maps [*, P, K] (or materialised probs)
+  const float* probs;          // MODE_PV input [N*H, P, K]
+  const uint8_t* key_mask;     // optional [N, K]
+  int store_accumulate;
+  int qk_src[P2P_MAX_BATCH];
+  int store_slot[P2P_MAX_BATCH];
+};
+
+struct CrossArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  int64_t ldq, ldk, ldv, ldo;
+  int64_t bsq, bsk, bsv, bso;
+  int N, P, K, H;
+  float scale_log2;
+  int n_qtiles;
+  float* store;
+  int store_accumulate;
+  int store_slot[P2P_MAX_BATCH];
+  int grp_first[P2P_MAX_GROUPS];
+  int grp_count[P2P_MAX_GROUPS];
+  const void* grp_prog[P2P_MAX_GROUPS];
+  const float* grp_alpha[P2P_MAX_GROUPS];
+};
+
+enum { MODE_FUSED_ = 0, MODE_STORE_ = 1, MODE_PROBS_ = 2, MODE_PV_ = 3 };
+
+int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st);
+int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, int n_groups, hipStream_t st);
+int run_localblend(const p2p_blend_args& a, hipStream_t st);
+int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
+
+}  // namespace p2p

@@ -1,0 +1,253 @@
+"""ctypes binding of ``libp2p_hip.so`` (C ABI: ``include/p2p_hip.h``).
+
+This module is the only place the product talks to the device kernels.  There is no
+fallback: if the shared library is missing or a call is rejected, it raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libp2p_hip.so")
+_lib = None
+
+# Optional launch observer (bench.py times the dominant kernel with HIP events through it):
+# an object with before(kind, tensors) / after(kind, tensors), called around each launch.
+LAUNCH_OBSERVER = None
+
+P2P_DTYPE_F32 = 0
+P2P_DTYPE_BF16 = 1
+P2P_COMPUTE_BF16 = 0
+P2P_COMPUTE_F32 = 1
+MAX_BATCH = 64
+MAX_GROUPS = 32
+MAX_KEYS_CROSS = 96
+PROGRAM_COLS = 128
+ABI_VERSION = 1
+
+
+class HipError(RuntimeError):
+    pass
+
+
+class AttnTensors(ctypes.Structure):
+    _fields_ = [
+        ("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("o", ctypes.c_void_p),
+        ("q_row_stride", ctypes.c_int64), ("k_row_stride", ctypes.c_int64),
+        ("v_row_stride", ctypes.c_int64), ("o_row_stride", ctypes.c_int64),
+        ("q_batch_stride", ctypes.c_int64), ("k_batch_stride", ctypes.c_int64),
+        ("v_batch_stride", ctypes.c_int64), ("o_batch_stride", ctypes.c_int64),
+        ("n_batch", ctypes.c_int32), ("n_query", ctypes.c_int32), ("n_key", ctypes.c_int32),
+        ("n_heads", ctypes.c_int32), ("head_dim", ctypes.c_int32),
+        ("io_dtype", ctypes.c_int32), ("compute", ctypes.c_int32),
+        ("scale", ctypes.c_float),
+    ]
+
+
+class Group(ctypes.Structure):
+    _fields_ = [("first", ctypes.c_int32), ("count", ctypes.c_int32),
+                ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p)]
+
+
+class BlendArgs(ctypes.Structure):
+    _fields_ = [
+        ("maps", ctypes.c_void_p * 8), ("n_maps", ctypes.c_int32), ("heads_per_map", ctypes.c_int32),
+        ("n_prompts", ctypes.c_int32), ("n_words", ctypes.c_int32), ("map_res", ctypes.c_int32),
+        ("alpha_layers", ctypes.c_void_p), ("substruct_layers", ctypes.c_void_p),
+        ("th_pool", ctypes.c_float), ("th_sub", ctypes.c_float),
+        ("x_t", ctypes.c_void_p), ("channels", ctypes.c_int32), ("lat_h", ctypes.c_int32),
+        ("lat_w", ctypes.c_int32), ("word_sums", ctypes.c_void_p), ("mask_out", ctypes.c_void_p),
+    ]
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def lib():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise HipError(f"{_LIB_PATH} is missing: run __graft_entry__.build() (make -C prompt-to-prompt_amd/csrc)")
+        L = ctypes.CDLL(_LIB_PATH)
+        i32, vp, f32, i64 = ctypes.c_int32, ctypes.c_void_p, ctypes.c_float, ctypes.c_int64
+        L.p2p_abi_version.restype = ctypes.c_int
+        L.p2p_error_string.restype = ctypes.c_char_p
+        L.p2p_error_string.argtypes = [ctypes.c_int]
+        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp]
+        L.p2p_cross_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, i32, vp, vp, i32, vp]
+        L.p2p_attn_probs.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp]
+        L.p2p_attn_pv.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
+        L.p2p_localblend.argtypes = [ctypes.POINTER(BlendArgs), vp]
+        L.p2p_store_scale.argtypes = [vp, vp, f32, i64, vp]
+        for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
+                   "p2p_localblend", "p2p_store_scale"):
+            getattr(L, fn).restype = ctypes.c_int
+        if L.p2p_abi_version() != ABI_VERSION:
+            raise HipError(f"libp2p_hip.so ABI {L.p2p_abi_version()} != {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
+                    "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale")
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().p2p_error_string(rc).decode()
+        raise HipError(f"{what} failed: {msg} (code {rc})")
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return P2P_DTYPE_F32
+    if t.dtype == torch.bfloat16:
+        return P2P_DTYPE_BF16
+    raise HipError(f"unsupported attention dtype {t.dtype} (float32 or bfloat16)")
+
+
+_COMPUTE = {"bf16": P2P_COMPUTE_BF16, "f32": P2P_COMPUTE_F32}
+
+
+def _require_cuda(*ts: Optional[torch.Tensor]):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise HipError("p2p_amd kernels need GPU tensors (no CPU path in the product)")
+
+
+def make_tensors(q, k, v, o, heads: int, scale: float, compute: str) -> AttnTensors:
+    """q/o: [N, P, H*d]; k/v: [N, K, H*d]; last dim contiguous."""
+    ref = q if q is not None else v
+    _require_cuda(q, k, v, o)
+    for t in (q, k, v, o):
+        if t is not None and (t.dim() != 3 or t.stride(-1) != 1):
+            raise HipError("attention operands must be [batch, tokens, heads*dim] with a unit last stride")
+    C = ref.shape[-1]
+    if C % heads:
+        raise HipError(f"channels {C} not divisible by heads {heads}")
+    t = AttnTensors()
+
+    def ptr(x):
+        return x.data_ptr() if x is not None else None
+
+    t.q, t.k, t.v, t.o = ptr(q), ptr(k), ptr(v), ptr(o)
+    z = lambda x, i: x.stride(i) if x is not None else 0  # noqa: E731
+    t.q_row_stride, t.k_row_stride, t.v_row_stride, t.o_row_stride = z(q, 1), z(k, 1), z(v, 1), z(o, 1)
+    t.q_batch_stride, t.k_batch_stride, t.v_batch_stride, t.o_batch_stride = z(q, 0), z(k, 0), z(v, 0), z(o, 0)
+    t.n_batch = ref.shape[0]
+    t.n_query = (q if q is not None else o).shape[1]
+    t.n_key = (k if k is not None else v).shape[1]
+    t.n_heads = heads
+    t.head_dim = C // heads
+    t.io_dtype = _dtype_code(ref)
+    t.compute = _COMPUTE[compute]
+    t.scale = float(scale)
+    return t
+
+
+def _i32_array(vals: Sequence[int]):
+    arr = (ctypes.c_int32 * len(vals))(*[int(x) for x in vals])
+    return arr
+
+
+def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None, store_slot=None,
+              accumulate=False):
+    t = make_tensors(q, k, v, o, heads, scale, compute)
+    src = _i32_array(qk_src) if qk_src is not None else None
+    slots = _i32_array(store_slot) if store_slot is not None else None
+    if store is not None:
+        _require_cuda(store)
+        assert store.dtype == torch.float32 and store.is_contiguous()
+    obs = LAUNCH_OBSERVER
+    if obs is not None:
+        obs.before("self", t)
+    rc = lib().p2p_self_attn_fwd(ctypes.byref(t), src, store.data_ptr() if store is not None else None,
+                                 slots, int(bool(accumulate)), _stream(q.device))
+    if obs is not None:
+        obs.after("self", t)
+    _check(rc, "p2p_self_attn_fwd")
+
+
+def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, store_slot=None,
+               accumulate=False):
+    """groups: list of (first, count, program_tensor|None, alpha_tensor|None)."""
+    t = make_tensors(q, k, v, o, heads, scale, compute)
+    G = (Group * len(groups))()
+    for i, (first, count, prog, alpha) in enumerate(groups):
+        G[i].first, G[i].count = int(first), int(count)
+        G[i].program = prog.data_ptr() if prog is not None else None
+        G[i].alpha = alpha.data_ptr() if alpha is not None else None
+    slots = _i32_array(store_slot) if store_slot is not None else None
+    if store is not None:
+        _require_cuda(store)
+        assert store.dtype == torch.float32 and store.is_contiguous()
+    obs = LAUNCH_OBSERVER
+    if obs is not None:
+        obs.before("cross", t)
+    rc = lib().p2p_cross_attn_fwd(ctypes.byref(t), G, len(groups),
+                                  store.data_ptr() if store is not None else None, slots,
+                                  int(bool(accumulate)), _stream(q.device))
+    if obs is not None:
+        obs.after("cross", t)
+    _check(rc, "p2p_cross_attn_fwd")
+
+
+def attn_probs(q, k, heads, scale, probs, compute="bf16", key_mask=None):
+    t = make_tensors(q, k, None, None, heads, scale, compute)
+    _require_cuda(probs, key_mask)
+    assert probs.dtype == torch.float32 and probs.is_contiguous()
+    rc = lib().p2p_attn_probs(ctypes.byref(t), key_mask.data_ptr() if key_mask is not None else None,
+                              probs.data_ptr(), _stream(q.device))
+    _check(rc, "p2p_attn_probs")
+
+
+def attn_pv(probs, v, o, heads, compute="bf16"):
+    t = make_tensors(None, None, v, o, heads, 1.0, compute)
+    t.n_query = o.shape[1]
+    _require_cuda(probs)
+    assert probs.dtype == torch.float32 and probs.is_contiguous()
+    rc = lib().p2p_attn_pv(ctypes.byref(t), probs.data_ptr(), _stream(v.device))
+    _check(rc, "p2p_attn_pv")
+
+
+def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_sub, x_t, word_sums,
+               mask_out=None):
+    _require_cuda(x_t, alpha_layers, word_sums, substruct_layers, mask_out, *maps)
+    a = BlendArgs()
+    for i, m in enumerate(maps):
+        assert m.dtype == torch.float32 and m.is_contiguous()
+        a.maps[i] = m.data_ptr()
+    B, W = alpha_layers.shape
+    a.n_maps = len(maps)
+    a.heads_per_map = heads_per_map
+    a.n_prompts = B
+    a.n_words = W
+    a.map_res = int(round((maps[0].shape[1]) ** 0.5))
+    a.alpha_layers = alpha_layers.data_ptr()
+    a.substruct_layers = substruct_layers.data_ptr() if substruct_layers is not None else None
+    a.th_pool, a.th_sub = float(th_pool), float(th_sub)
+    assert x_t.dtype == torch.float32 and x_t.is_contiguous()
+    a.x_t = x_t.data_ptr()
+    a.channels, a.lat_h, a.lat_w = x_t.shape[1], x_t.shape[2], x_t.shape[3]
+    a.word_sums = word_sums.data_ptr()
+    a.mask_out = mask_out.data_ptr() if mask_out is not None else None
+    rc = lib().p2p_localblend(ctypes.byref(a), _stream(x_t.device))
+    _check(rc, "p2p_localblend")
+
+
+def store_scale(src: torch.Tensor, divisor: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _require_cuda(src)
+    assert src.dtype == torch.float32 and src.is_contiguous()
+    out = torch.empty_like(src) if out is None else out
+    rc = lib().p2p_store_scale(src.data_ptr(), out.data_ptr(), float(divisor), src.numel(), _stream(src.device))
+    _check(rc, "p2p_store_scale")
+    return out

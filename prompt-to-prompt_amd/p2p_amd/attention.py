@@ -1,0 +1,59 @@
+"""Attention entry points used by the patched ``CrossAttention.forward``.
+
+* ``plain_attention``        -- no controller work (``DummyController``, uncond passes);
+* ``materialized_attention`` -- the reference protocol for controllers that edit a
+  materialised probability tensor (``controller(attn, is_cross, place)``,
+  ptp_utils.py:204-206): probabilities and P.V both run as HIP kernels, the controller
+  sees an f32 ``[N*H, P, K]`` tensor exactly like the reference's.
+
+Fused controllers (this package's AttentionStore / AttentionControlEdit family) bypass
+both and launch one edit-aware kernel per call (controllers.py).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+from . import config
+
+
+def _singles(n):
+    return [(i, 1, None, None) for i in range(n)]
+
+
+def plain_attention(q, k, v, heads, scale, out=None):
+    out = torch.empty_like(q) if out is None else out
+    if k.shape[1] <= _hip.MAX_KEYS_CROSS and q.shape[0] <= _hip.MAX_GROUPS:
+        _hip.cross_attn(q, k, v, out, heads, scale, _singles(q.shape[0]), compute=config.COMPUTE)
+    else:
+        _hip.self_attn(q, k, v, out, heads, scale, compute=config.COMPUTE)
+    return out
+
+
+def attention_probs(q, k, heads, scale, mask=None):
+    """softmax(Q K^T * scale) as [N*H, P, K] f32 (ptp_utils.py:195-204)."""
+    N, P, _ = q.shape
+    K = k.shape[1]
+    probs = torch.empty(N * heads, P, K, dtype=torch.float32, device=q.device)
+    key_mask = None
+    if mask is not None:
+        key_mask = mask.reshape(N, -1).to(device=q.device, dtype=torch.uint8).contiguous()
+        if key_mask.shape[1] != K:
+            raise ValueError(f"mask has {key_mask.shape[1]} keys, attention has {K}")
+    _hip.attn_probs(q, k, heads, scale, probs, compute=config.COMPUTE, key_mask=key_mask)
+    return probs
+
+
+def attention_pv(probs, v, heads, n_query, out_dtype):
+    N = v.shape[0]
+    out = torch.empty(N, n_query, v.shape[2], dtype=out_dtype, device=v.device)
+    _hip.attn_pv(probs.contiguous(), v, out, heads, compute=config.COMPUTE)
+    return out
+
+
+def materialized_attention(controller, q, k, v, heads, scale, is_cross, place_in_unet, mask=None):
+    probs = attention_probs(q, k, heads, scale, mask)
+    probs = controller(probs, is_cross, place_in_unet)
+    if probs.dtype != torch.float32:
+        probs = probs.float()
+    return attention_pv(probs, v, heads, q.shape[1], q.dtype)

@@ -1,0 +1,498 @@
+"""Prompt-to-Prompt attention controllers -- the reference API, fused underneath.
+
+Public surface of ``main.py:33-307`` (same class names, constructor arguments, attributes
+and ``__call__`` / ``forward`` / ``step_callback`` / ``between_steps`` / ``reset`` /
+``get_average_attention`` protocol).  The difference is underneath: when the patched
+``CrossAttention.forward`` (ptp_utils.register_attention_control) finds one of these
+controllers, it calls :meth:`AttentionControl.attention`, which launches ONE HIP kernel per
+call that computes the attention with the controller's edit and store fused in:
+
+* self-attention: flash kernel; source-map injection as a batch index remap;
+* cross-attention: exact-softmax kernel; Replace / Refine / Reweight as a device edit
+  program (programs.py) applied between softmax and PV;
+* AttentionStore: probabilities written (step 0) or added (later steps) to the running-sum
+  tensors in the kernel epilogue, only for the maps the reference keeps (P <= 32**2).
+
+A subclass that overrides any method the fused kernel encodes (``forward``,
+``replace_cross_attention``, ``replace_self_attention``, ``__call__``) gets the reference
+protocol instead: the probabilities are materialised by a HIP kernel, handed to
+``controller(attn, is_cross, place_in_unet)`` and multiplied by V by a second HIP kernel.
+"""
+from __future__ import annotations
+
+import abc
+from collections import defaultdict
+from typing import Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _hip
+from . import config
+from . import programs
+from . import seq_aligner
+from .attention import materialized_attention, plain_attention
+from .ptp_words import get_time_words_attention_alpha, get_word_inds
+from .tokenizer import default_tokenizer
+
+NUM_DIFFUSION_STEPS = 100   # main.py:19
+GUIDANCE_SCALE = 7.5        # main.py:20
+MAX_NUM_WORDS = 77          # main.py:21
+MAX_STORED_QUERIES = 32 ** 2  # main.py:131
+
+_tokenizer = None
+
+
+def set_tokenizer(tokenizer):
+    """The reference reads a module-global ``tokenizer`` (main.py:30); this sets ours."""
+    global _tokenizer
+    _tokenizer = tokenizer
+
+
+def get_tokenizer():
+    return _tokenizer if _tokenizer is not None else default_tokenizer()
+
+
+def default_device() -> torch.device:
+    return torch.device("cuda:0") if torch.cuda.is_available() else torch.device("cpu")
+
+
+def _low_resource() -> bool:
+    return bool(config.LOW_RESOURCE)
+
+
+class NotFusable(Exception):
+    """Raised while planning a fused call that the kernels cannot express."""
+
+
+# ============================================================================ LocalBlend
+def fused_local_blend(x_t, attention_store, alpha_flat, sub_flat, th_pool, th_sub):
+    """LocalBlend on the running-sum store with the HIP blend kernels (returns a new x_t)."""
+    maps = list(attention_store["down_cross"][2:4]) + list(attention_store["up_cross"][:3])
+    B = alpha_flat.shape[0]
+    if len(maps) != 5:
+        raise ValueError(f"LocalBlend needs 2 down and 3 up 16x16 cross maps, store has {len(maps)}")
+    heads = maps[0].shape[0] // B
+    maps = [m if (m.dtype == torch.float32 and m.is_contiguous()) else m.float().contiguous() for m in maps]
+    out = x_t.to(torch.float32).contiguous().clone()
+    ws = torch.empty(B * 2 * len(maps) * heads * maps[0].shape[1], dtype=torch.float32, device=out.device)
+    _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, out, ws)
+    return out.to(x_t.dtype)
+
+
+def _word_alpha_layers(prompts, words, tokenizer, n_words=MAX_NUM_WORDS):
+    a = torch.zeros(len(prompts), 1, 1, 1, 1, n_words)
+    for i, (prompt, ws) in enumerate(zip(prompts, words)):
+        for word in ([ws] if type(ws) is str else ws):
+            a[i, :, :, :, :, get_word_inds(prompt, word, tokenizer)] = 1
+    return a
+
+
+class LocalBlend:
+    """main.py:33-66.  Valid for two prompts only, as in the reference (its mask
+    ``mask[:1] + mask[1:]`` does not broadcast for more); use null_text.LocalBlend for B > 2."""
+
+    def __call__(self, x_t, attention_store):
+        if self.alpha_layers.shape[0] != 2:
+            raise ValueError("main-form LocalBlend broadcasts only for 2 prompts (see null_text.LocalBlend)")
+        return fused_local_blend(x_t, attention_store, self._alpha_flat, None, self.threshold, self.threshold)
+
+    def __init__(self, prompts: List[str], words, threshold=.3, tokenizer=None, device=None):
+        tokenizer = tokenizer or get_tokenizer()
+        device = device or default_device()
+        self.alpha_layers = _word_alpha_layers(prompts, words, tokenizer).to(device)
+        self._alpha_flat = self.alpha_layers.reshape(len(prompts), -1).contiguous()
+        self.threshold = threshold
+
+
+# ============================================================================ controllers
+class AttentionControl(abc.ABC):
+    """main.py:69-107 -- step/layer counters and the cond-half dispatch."""
+
+    _NATIVE = ("__call__",)
+
+    def step_callback(self, x_t):
+        return x_t
+
+    def between_steps(self):
+        return
+
+    @property
+    def num_uncond_att_layers(self):
+        return self.num_att_layers if _low_resource() else 0
+
+    @abc.abstractmethod
+    def forward(self, attn, is_cross: bool, place_in_unet: str):
+        raise NotImplementedError
+
+    def __call__(self, attn, is_cross: bool, place_in_unet: str):
+        if self.cur_att_layer >= self.num_uncond_att_layers:
+            if _low_resource():
+                attn = self.forward(attn, is_cross, place_in_unet)
+            else:
+                half = attn.shape[0] // 2
+                attn[half:] = self.forward(attn[half:], is_cross, place_in_unet)
+        self._advance_layer()
+        return attn
+
+    def _advance_layer(self):
+        self.cur_att_layer += 1
+        if self.cur_att_layer == self.num_att_layers + self.num_uncond_att_layers:
+            self.cur_att_layer = 0
+            self.cur_step += 1
+            self.between_steps()
+
+    def reset(self):
+        self.cur_step = 0
+        self.cur_att_layer = 0
+
+    def __init__(self):
+        self.cur_step = 0
+        self.num_att_layers = -1
+        self.cur_att_layer = 0
+
+    # ------------------------------------------------------------------ fused protocol
+    def fused_supported(self) -> bool:
+        """True when every method the fused kernels encode is this library's own."""
+        cls = type(self)
+        names = set()
+        for owner in cls.__mro__:
+            names.update(owner.__dict__.get("_NATIVE", ()))
+        for name in names:
+            # the class that resolves `name` must be one of ours
+            for owner in cls.__mro__:
+                if name in owner.__dict__:
+                    if not owner.__dict__.get("_P2P_LIB", False):
+                        return False
+                    break
+        return True
+
+    def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
+        raise NotFusable
+
+    def attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask=None):
+        """Called by the patched CrossAttention.forward with the projections q, k, v."""
+        if mask is None and self.fused_supported():
+            try:
+                if self.cur_att_layer >= self.num_uncond_att_layers:
+                    out = self._fused_forward(q, k, v, heads, scale, is_cross, place_in_unet)
+                else:
+                    out = plain_attention(q, k, v, heads, scale)
+                self._advance_layer()
+                return out
+            except NotFusable:
+                pass
+        return materialized_attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask)
+
+    def _cond_start(self, n_batch: int) -> int:
+        return 0 if _low_resource() else n_batch // 2
+
+
+AttentionControl._P2P_LIB = True
+
+
+class EmptyControl(AttentionControl):
+    """main.py:110-113."""
+
+    _NATIVE = ("forward",)
+
+    def forward(self, attn, is_cross: bool, place_in_unet: str):
+        return attn
+
+    def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
+        return plain_attention(q, k, v, heads, scale)
+
+
+EmptyControl._P2P_LIB = True
+
+
+class AttentionStore(AttentionControl):
+    """main.py:116-159.  ``store_self_maps = False`` keeps only the cross maps (the ones
+    LocalBlend and ``show_cross_attention`` read); the default matches the reference."""
+
+    _NATIVE = ("forward", "between_steps")
+    store_self_maps = True
+
+    @staticmethod
+    def get_empty_store():
+        return {"down_cross": [], "mid_cross": [], "up_cross": [],
+                "down_self": [], "mid_self": [], "up_self": []}
+
+    def forward(self, attn, is_cross: bool, place_in_unet: str):
+        key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
+        if attn.shape[1] <= MAX_STORED_QUERIES:
+            self.step_store[key].append(attn)
+        return attn
+
+    def between_steps(self):
+        if len(self.attention_store) == 0:
+            self.attention_store = self.step_store
+        else:
+            # fused calls already added their maps in the kernel epilogue; only maps handed
+            # over through the materialised protocol are still pending here
+            for key, items in self.step_store.items():
+                for i, item in enumerate(items):
+                    self.attention_store[key][i] += item
+        self.step_store = self.get_empty_store()
+        self._fused_calls = defaultdict(int)
+
+    def get_average_attention(self):
+        def avg(item):
+            if item.is_cuda and item.dtype == torch.float32 and item.is_contiguous():
+                return _hip.store_scale(item, float(self.cur_step))
+            return item / self.cur_step
+        return {key: [avg(item) for item in self.attention_store[key]] for key in self.attention_store}
+
+    def reset(self):
+        super().reset()
+        self.step_store = self.get_empty_store()
+        self.attention_store = {}
+        self._fused_calls = defaultdict(int)
+
+    def __init__(self):
+        super().__init__()
+        self.step_store = self.get_empty_store()
+        self.attention_store = {}
+        self._fused_calls = defaultdict(int)
+
+    # ------------------------------------------------------------------ fused store
+    def _store_target(self, is_cross, place_in_unet, n_cond, heads, P, K, device):
+        """Running-sum tensor this call's maps go to, and whether to add or overwrite."""
+        if P > MAX_STORED_QUERIES or (not is_cross and not self.store_self_maps):
+            return None, False
+        key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
+        idx = self._fused_calls[key]
+        self._fused_calls[key] = idx + 1
+        if len(self.attention_store) == 0:
+            t = torch.empty(n_cond * heads, P, K, dtype=torch.float32, device=device)
+            self.step_store[key].append(t)
+            return t, False
+        return self.attention_store[key][idx], True
+
+    def _slots(self, n_batch, n0, heads, store):
+        if store is None:
+            return None
+        return [-1] * n0 + [(n - n0) * heads for n in range(n0, n_batch)]
+
+    def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
+        N, P, K = q.shape[0], q.shape[1], k.shape[1]
+        n0 = self._cond_start(N)
+        store, acc = self._store_target(is_cross, place_in_unet, N - n0, heads, P, K, q.device)
+        slots = self._slots(N, n0, heads, store)
+        out = torch.empty_like(q)
+        if is_cross and K <= _hip.MAX_KEYS_CROSS and N <= _hip.MAX_GROUPS:
+            groups = [(n, 1, None, None) for n in range(N)]
+            _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
+                            store_slot=slots, accumulate=acc)
+        else:
+            _hip.self_attn(q, k, v, out, heads, scale, compute=config.COMPUTE, store=store,
+                           store_slot=slots, accumulate=acc)
+        return out
+
+
+AttentionStore._P2P_LIB = True
+
+
+class AttentionControlEdit(AttentionStore, abc.ABC):
+    """main.py:162-212."""
+
+    _NATIVE = ("forward", "replace_self_attention", "_replace_self")
+    SELF_REPLACE_MAX_KEYS = 16 ** 2   # main.py:170 (null_text.py:225 uses 32 ** 2)
+
+    def step_callback(self, x_t):
+        if self.local_blend is not None:
+            x_t = self.local_blend(x_t, self.attention_store)
+        return x_t
+
+    def replace_self_attention(self, attn_base, att_replace):
+        if att_replace.shape[2] <= self.SELF_REPLACE_MAX_KEYS:
+            return attn_base.unsqueeze(0).expand(att_replace.shape[0], *attn_base.shape)
+        return att_replace
+
+    @abc.abstractmethod
+    def replace_cross_attention(self, attn_base, att_replace):
+        raise NotImplementedError
+
+    def _in_self_window(self) -> bool:
+        return self.num_self_replace[0] <= self.cur_step < self.num_self_replace[1]
+
+    def _replace_self(self, attn_base, att_replace, place_in_unet):
+        return self.replace_self_attention(attn_base, att_replace)
+
+    def forward(self, attn, is_cross: bool, place_in_unet: str):
+        """Reference protocol on a materialised [B*H, P, K] tensor (main.py:180-197)."""
+        AttentionStore.forward(self, attn, is_cross, place_in_unet)
+        if not (is_cross or self._in_self_window()):
+            return attn
+        per_prompt = attn.reshape(self.batch_size, attn.shape[0] // self.batch_size, *attn.shape[1:])
+        base, edits = per_prompt[0], per_prompt[1:]
+        if is_cross:
+            a = self.cross_replace_alpha[self.cur_step]
+            per_prompt[1:] = self.replace_cross_attention(base, edits) * a + (1 - a) * edits
+        else:
+            per_prompt[1:] = self._replace_self(base, edits, place_in_unet)
+        return per_prompt.reshape(attn.shape[0], *attn.shape[1:])
+
+    def __init__(self, prompts, num_steps: int,
+                 cross_replace_steps: Union[float, Tuple[float, float], Dict[str, Tuple[float, float]]],
+                 self_replace_steps: Union[float, Tuple[float, float]],
+                 local_blend: Optional[LocalBlend], tokenizer=None, device=None):
+        super().__init__()
+        self.tokenizer = tokenizer or get_tokenizer()
+        self.device = device or default_device()
+        self.batch_size = len(prompts)
+        self.cross_replace_alpha = get_time_words_attention_alpha(
+            prompts, num_steps, cross_replace_steps, self.tokenizer).to(self.device)
+        if type(self_replace_steps) is float:
+            self_replace_steps = 0, self_replace_steps
+        self.num_self_replace = int(num_steps * self_replace_steps[0]), int(num_steps * self_replace_steps[1])
+        self.local_blend = local_blend
+        self._program_cache = {}
+
+    # ------------------------------------------------------------------ fused edits
+    def _edit_program(self) -> programs.EditProgram:
+        raise NotFusable
+
+    def _device_program(self, device):
+        key = str(device)
+        if key not in self._program_cache:
+            self._program_cache[key] = self._edit_program().to_device(device)
+        return self._program_cache[key]
+
+    def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
+        N, P, K = q.shape[0], q.shape[1], k.shape[1]
+        n0 = self._cond_start(N)
+        n_cond = N - n0
+        if n_cond != self.batch_size:
+            raise ValueError(f"controller built for {self.batch_size} prompts got a batch of {n_cond}")
+        if is_cross:
+            alpha = self.cross_replace_alpha[self.cur_step]
+            if (K > _hip.MAX_KEYS_CROSS or alpha.shape[-1] != K or n0 + 1 > _hip.MAX_GROUPS
+                    or alpha.device != q.device):
+                raise NotFusable
+            prog = self._device_program(q.device)
+        store, acc = self._store_target(is_cross, place_in_unet, n_cond, heads, P, K, q.device)
+        slots = self._slots(N, n0, heads, store)
+        out = torch.empty_like(q)
+        if is_cross:
+            groups = [(n, 1, None, None) for n in range(n0)] + [(n0, n_cond, prog, alpha.contiguous())]
+            _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
+                            store_slot=slots, accumulate=acc)
+        else:
+            qk_src = None
+            if self._in_self_window() and K <= self.SELF_REPLACE_MAX_KEYS:
+                qk_src = list(range(N))
+                for n in range(n0 + 1, N):
+                    qk_src[n] = n0       # P_edit <- P_source, V stays the edit's own
+            _hip.self_attn(q, k, v, out, heads, scale, compute=config.COMPUTE, qk_src=qk_src, store=store,
+                           store_slot=slots, accumulate=acc)
+        return out
+
+
+AttentionControlEdit._P2P_LIB = True
+
+
+class AttentionReplace(AttentionControlEdit):
+    """main.py:215-230."""
+
+    _NATIVE = ("replace_cross_attention",)
+
+    def replace_cross_attention(self, attn_base, att_replace):
+        return torch.einsum('hpw,bwn->bhpn', attn_base, self.mapper)
+
+    def _edit_program(self):
+        return programs.replace_program(self.mapper)
+
+    def __init__(self, prompts, num_steps: int, cross_replace_steps: float, self_replace_steps: float,
+                 local_blend: Optional[LocalBlend] = None, tokenizer=None, device=None):
+        super().__init__(prompts, num_steps, cross_replace_steps, self_replace_steps, local_blend,
+                         tokenizer, device)
+        self.mapper = seq_aligner.get_replacement_mapper(prompts, self.tokenizer).to(self.device)
+
+
+AttentionReplace._P2P_LIB = True
+
+
+class AttentionRefine(AttentionControlEdit):
+    """main.py:233-253."""
+
+    _NATIVE = ("replace_cross_attention",)
+
+    def replace_cross_attention(self, attn_base, att_replace):
+        gathered = attn_base[:, :, self.mapper].permute(2, 0, 1, 3)
+        return gathered * self.alphas + att_replace * (1 - self.alphas)
+
+    def _edit_program(self):
+        return programs.refine_program(self.mapper, self.alphas)
+
+    def __init__(self, prompts, num_steps: int, cross_replace_steps: float, self_replace_steps: float,
+                 local_blend: Optional[LocalBlend] = None, tokenizer=None, device=None):
+        super().__init__(prompts, num_steps, cross_replace_steps, self_replace_steps, local_blend,
+                         tokenizer, device)
+        mapper, alphas = seq_aligner.get_refinement_mapper(prompts, self.tokenizer)
+        self.mapper, alphas = mapper.to(self.device), alphas.to(self.device)
+        self.alphas = alphas.reshape(alphas.shape[0], 1, 1, alphas.shape[1])
+
+
+AttentionRefine._P2P_LIB = True
+
+
+class AttentionReweight(AttentionControlEdit):
+    """main.py:256-278 (optionally chained on a Replace / Refine controller)."""
+
+    _NATIVE = ("replace_cross_attention",)
+
+    def replace_cross_attention(self, attn_base, att_replace):
+        if self.prev_controller is not None:
+            attn_base = self.prev_controller.replace_cross_attention(attn_base, att_replace)
+        return attn_base[None, :, :, :] * self.equalizer[:, None, None, :]
+
+    def _edit_program(self):
+        inner = None
+        prev = self.prev_controller
+        if prev is not None:
+            if not (isinstance(prev, AttentionControlEdit) and prev.fused_supported()):
+                raise NotFusable
+            inner = prev._edit_program()
+            if not np.all(inner.post == 1.0):
+                raise NotFusable
+        return programs.reweight_program(self.equalizer, self.batch_size - 1, inner)
+
+    def __init__(self, prompts, num_steps: int, cross_replace_steps: float, self_replace_steps: float,
+                 equalizer, local_blend: Optional[LocalBlend] = None,
+                 controller: Optional[AttentionControlEdit] = None, tokenizer=None, device=None):
+        super().__init__(prompts, num_steps, cross_replace_steps, self_replace_steps, local_blend,
+                         tokenizer, device)
+        self.equalizer = equalizer.to(self.device)
+        self.prev_controller = controller
+
+
+AttentionReweight._P2P_LIB = True
+
+
+def get_equalizer(text: str, word_select: Union[int, Tuple[int, ...]],
+                  values: Union[List[float], Tuple[float, ...]], tokenizer=None):
+    """main.py:281-290: one row per value, every selected word's columns set to ``values``."""
+    tokenizer = tokenizer or get_tokenizer()
+    if type(word_select) is int or type(word_select) is str:
+        word_select = (word_select,)
+    eq = torch.ones(len(values), MAX_NUM_WORDS)
+    vals = torch.tensor(values, dtype=torch.float32)
+    for word in word_select:
+        eq[:, get_word_inds(text, word, tokenizer)] = vals
+    return eq
+
+
+def aggregate_attention(attention_store: AttentionStore, res: int, from_where: List[str], is_cross: bool,
+                        select: int, prompts: Optional[List[str]] = None):
+    """main.py:293-307 (``prompts`` is the reference's module global; defaults to the
+    controller's batch size)."""
+    n_prompts = len(prompts) if prompts is not None else attention_store.batch_size
+    maps = attention_store.get_average_attention()
+    picked = []
+    for location in from_where:
+        for item in maps[f"{location}_{'cross' if is_cross else 'self'}"]:
+            if item.shape[1] == res ** 2:
+                picked.append(item.reshape(n_prompts, -1, res, res, item.shape[-1])[select])
+    out = torch.cat(picked, dim=0)
+    return (out.sum(0) / out.shape[0]).cpu()

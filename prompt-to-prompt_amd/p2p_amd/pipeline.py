@@ -1,0 +1,83 @@
+"""Synthetic SD-v1.4 pipeline: the callers around the hot path (sampling loop inputs).
+
+No checkpoints, tokenizer vocabularies or text encoders are available offline, so the
+"model" object that ptp_utils.text2image_ldm_stable expects (``tokenizer``,
+``text_encoder``, ``unet``, ``scheduler``, ``device``; main.py:29) is assembled from
+stand-ins: the deterministic tokenizer, a seeded embedding-table text encoder that maps
+identical prompts to identical contexts (as CLIP does for the shared "" uncond rows), the
+random-init SD-shaped U-Net and the DDIM scheduler of null_text.py:16-20.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from .ddim import DDIMScheduler
+from .tokenizer import default_tokenizer
+from .unet import UNet2DConditionModel
+
+VOCAB = 49408
+
+
+class SyntheticTextEncoder(nn.Module):
+    def __init__(self, dim=768, max_len=77, seed=1):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.register_buffer("token", torch.randn(VOCAB, dim, generator=g))
+        self.register_buffer("pos", 0.1 * torch.randn(max_len, dim, generator=g))
+
+    def forward(self, ids):
+        return (self.token[ids] + self.pos[None, : ids.shape[1]],)
+
+
+class SyntheticStableDiffusion:
+    def __init__(self, device="cuda", dtype=torch.float32, seed=0):
+        self.device = torch.device(device)
+        self.tokenizer = default_tokenizer()
+        torch.manual_seed(seed)
+        self.unet = UNet2DConditionModel().to(self.device, dtype).eval()
+        for p in self.unet.parameters():
+            p.requires_grad_(False)
+        self.text_encoder = SyntheticTextEncoder().to(self.device)
+        self.scheduler = DDIMScheduler(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
+                                       clip_sample=False, set_alpha_to_one=False)
+        self.vae = None
+
+
+# The north-star workload (BASELINE.json configs[1]): 1 source + 3 single-word replacements.
+SOURCE = "a painting of a squirrel eating a burger"
+EDITS = ["a painting of a lion eating a burger", "a painting of a cat eating a burger",
+         "a painting of a squirrel eating a lasagna"]
+BLEND_WORDS = (("squirrel", "burger"), ("lion",), ("cat",), ("lasagna",))
+
+
+def north_star_prompts() -> List[str]:
+    return [SOURCE] + EDITS
+
+
+def seed_latent(seed: int) -> torch.Tensor:
+    """x_T exactly as main.py:427-428 draws it (CPU generator)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn((1, 4, 64, 64), generator=g)
+
+
+def make_replace_controller(prompts: Sequence[str], num_steps: int = 50, cross_replace_steps=0.8,
+                            self_replace_steps=0.4, blend_words=BLEND_WORDS, store_self_maps=False,
+                            device=None):
+    from . import null_text
+    lb = null_text.LocalBlend(list(prompts), blend_words, device=device) if blend_words is not None else None
+    ctrl = null_text.AttentionReplace(list(prompts), num_steps, cross_replace_steps=cross_replace_steps,
+                                      self_replace_steps=self_replace_steps, local_blend=lb, device=device)
+    ctrl.store_self_maps = store_self_maps
+    return ctrl
+
+
+@torch.no_grad()
+def run_edit_group(model: SyntheticStableDiffusion, prompts: Sequence[str], controller, x_T: torch.Tensor,
+                   num_steps: int = 50, guidance_scale: float = 7.5):
+    from . import ptp_utils
+    latents, _ = ptp_utils.text2image_ldm_stable(model, list(prompts), controller, num_inference_steps=num_steps,
+                                                 guidance_scale=guidance_scale, latent=x_T)
+    return latents

@@ -1,0 +1,114 @@
+"""Device edit programs for the fused cross-attention kernel.
+
+Every cross-attention edit of the reference is, per edit ``e`` and output word ``w``,
+
+    R[w]   = post[w] * ( c_rep[w] * P_e[w] + sum_t val[t] * P_0[row[t]] )     t in column w
+    P_e'   = alpha[w] * R[w] + (1 - alpha[w]) * P_e[w]
+
+with the rows/values stored as a compressed column list:
+
+* AttentionReplace  (main.py:217-218)  c_rep 0, column w of the mapper (``einsum('hpw,bwn')``);
+* AttentionRefine   (main.py:235-239)  c_rep 1 - a[w], one term (mapper[w] mod n, a[w]);
+  a ``-1`` mapper entry gathers column n-1 as torch's negative indexing does;
+* AttentionReweight (main.py:258-264)  c_rep 0, one term (w, eq[w]); chained on a Replace or
+  Refine controller it keeps the inner terms and sets post = eq.
+
+Zeros of the dense mapper are skipped, so the column sums are the reference's with the
+zero terms removed (exact for single-entry columns, which is every column the mapper
+builders produce except multi-token source words).
+
+Blob layout (int32/float32 words, P2P_PROGRAM_COLS = 128 column stride):
+    header  int32[4]  = n_edits, n_cols, nnz, 128
+    c_rep   f32 [n_edits][128]
+    post    f32 [n_edits][128]
+    colptr  i32 [n_edits][128]   (column w spans [colptr[w], colptr[w+1]) of the edit's terms)
+    rowidx  i32 [nnz]
+    val     f32 [nnz]
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+PROGRAM_COLS = 128
+
+
+@dataclass
+class EditProgram:
+    n_edits: int
+    n_cols: int
+    c_rep: np.ndarray               # [E, n_cols] f32
+    post: np.ndarray                # [E, n_cols] f32
+    terms: List[List[List[tuple]]] = field(default_factory=list)  # [E][w] -> [(row, val)]
+
+    def blob(self) -> np.ndarray:
+        E, n = self.n_edits, self.n_cols
+        if n + 1 > PROGRAM_COLS:
+            raise ValueError(f"{n} words exceed the program column stride {PROGRAM_COLS}")
+        c_rep = np.zeros((E, PROGRAM_COLS), np.float32)
+        post = np.zeros((E, PROGRAM_COLS), np.float32)
+        colptr = np.zeros((E, PROGRAM_COLS), np.int32)
+        rows, vals = [], []
+        for e in range(E):
+            c_rep[e, :n] = self.c_rep[e]
+            post[e, :n] = self.post[e]
+            for w in range(n):
+                colptr[e, w] = len(rows)
+                for (r, v) in self.terms[e][w]:
+                    rows.append(r)
+                    vals.append(v)
+            colptr[e, n:] = len(rows)
+        header = np.array([E, n, len(rows), PROGRAM_COLS], np.int32)
+        parts = [header.view(np.uint8), c_rep.view(np.uint8).ravel(), post.view(np.uint8).ravel(),
+                 colptr.view(np.uint8).ravel(), np.array(rows, np.int32).view(np.uint8),
+                 np.array(vals, np.float32).view(np.uint8)]
+        return np.concatenate(parts)
+
+    def to_device(self, device) -> torch.Tensor:
+        return torch.from_numpy(self.blob().copy()).to(device)
+
+
+def replace_program(mapper: torch.Tensor) -> EditProgram:
+    """mapper: [E, n, n] float (seq_aligner.get_replacement_mapper)."""
+    m = mapper.detach().to("cpu", torch.float32).numpy()
+    E, n, _ = m.shape
+    terms = []
+    for e in range(E):
+        cols = []
+        for w in range(n):
+            nz = np.nonzero(m[e, :, w])[0]
+            cols.append([(int(r), float(m[e, r, w])) for r in nz])
+        terms.append(cols)
+    return EditProgram(E, n, np.zeros((E, n), np.float32), np.ones((E, n), np.float32), terms)
+
+
+def refine_program(mapper: torch.Tensor, alphas: torch.Tensor) -> EditProgram:
+    """mapper: [E, n] int64 (may hold -1); alphas: [E, n] or [E, 1, 1, n] float."""
+    mp = mapper.detach().cpu().numpy().astype(np.int64)
+    a = alphas.detach().to("cpu", torch.float32).reshape(mp.shape).numpy()
+    E, n = mp.shape
+    c_rep = (np.float32(1.0) - a).astype(np.float32)   # torch: 1 - alphas in f32
+    terms = [[[(int(mp[e, w] % n), float(a[e, w]))] for w in range(n)] for e in range(E)]
+    return EditProgram(E, n, c_rep, np.ones((E, n), np.float32), terms)
+
+
+def reweight_program(equalizer: torch.Tensor, n_edits: int, inner: Optional[EditProgram]) -> EditProgram:
+    """equalizer: [E_eq, n] with E_eq in {1, n_edits} (broadcast of main.py:262-263)."""
+    eq = equalizer.detach().to("cpu", torch.float32).numpy()
+    if eq.ndim != 2 or eq.shape[0] not in (1, n_edits):
+        raise ValueError(f"equalizer of shape {tuple(eq.shape)} does not broadcast over {n_edits} edits")
+    n = eq.shape[1]
+    rows = [eq[e if eq.shape[0] > 1 else 0] for e in range(n_edits)]
+    if inner is None:
+        terms = [[[(w, float(rows[e][w]))] for w in range(n)] for e in range(n_edits)]
+        return EditProgram(n_edits, n, np.zeros((n_edits, n), np.float32), np.ones((n_edits, n), np.float32),
+                           terms)
+    if inner.n_edits != n_edits or inner.n_cols != n:
+        raise ValueError("chained controller has a different number of edits / words")
+    if not np.all(inner.post == 1.0):
+        raise ValueError("reweight chained on a reweight is not a fused program")
+    post = np.stack(rows).astype(np.float32)
+    return EditProgram(n_edits, n, inner.c_rep.copy(), post, inner.terms)

@@ -1,0 +1,163 @@
+"""Drop-in for the reference ``ptp_utils.py``: the attention hook, the sampling loop and the
+word/time tables.
+
+``register_attention_control(model, controller)`` keeps the reference's patching rule
+(every module whose class is named ``CrossAttention`` under ``unet.{down,mid,up}*``,
+ptp_utils.py:223-240) and its forward signature (``:183``), and sets
+``controller.num_att_layers`` (``:242``).  The replacement forward keeps the projections as
+they are and hands ``q, k, v`` to the controller's fused kernel (controllers.py) -- or, for a
+reference-style controller, to the materialised protocol (attention.py).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .attention import materialized_attention, plain_attention
+from .ptp_words import get_time_words_attention_alpha, get_word_inds, update_alpha_time_word  # noqa: F401
+
+
+# ------------------------------------------------------------------ sampling loop
+def diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource=False):
+    """One CFG denoising step (ptp_utils.py:65-76)."""
+    if low_resource:
+        eps_u = model.unet(latents, t, encoder_hidden_states=context[0])["sample"]
+        eps_c = model.unet(latents, t, encoder_hidden_states=context[1])["sample"]
+    else:
+        eps = model.unet(torch.cat([latents] * 2), t, encoder_hidden_states=context)["sample"]
+        eps_u, eps_c = eps.chunk(2)
+    noise_pred = eps_u + guidance_scale * (eps_c - eps_u)
+    latents = model.scheduler.step(noise_pred, t, latents)["prev_sample"]
+    return controller.step_callback(latents)
+
+
+def latent2image(vae, latents):
+    """ptp_utils.py:79-85 (needs a VAE; the synthetic pipeline has none)."""
+    latents = 1 / 0.18215 * latents
+    image = vae.decode(latents)["sample"]
+    image = (image / 2 + 0.5).clamp(0, 1)
+    image = image.cpu().permute(0, 2, 3, 1).numpy()
+    return (image * 255).astype(np.uint8)
+
+
+def init_latent(latent, model, height, width, generator, batch_size):
+    """ptp_utils.py:88-95: one x_T shared by every prompt of the group."""
+    if latent is None:
+        latent = torch.randn((1, model.unet.in_channels, height // 8, width // 8), generator=generator)
+    latents = latent.expand(batch_size, model.unet.in_channels, height // 8, width // 8).to(model.device)
+    return latent, latents
+
+
+def _encode(model, prompts, encoder):
+    ids = model.tokenizer(prompts, padding="max_length", max_length=model.tokenizer.model_max_length,
+                          truncation=True, return_tensors="pt").input_ids
+    return encoder(ids.to(model.device))[0]
+
+
+@torch.no_grad()
+def text2image_ldm(model, prompt: List[str], controller, num_inference_steps: int = 50,
+                   guidance_scale: Optional[float] = 7., generator: Optional[torch.Generator] = None,
+                   latent: Optional[torch.FloatTensor] = None):
+    """ptp_utils.py:98-126 (LDM-256: 32x32 latent, LDMBert context)."""
+    register_attention_control(model, controller)
+    height = width = 256
+    batch_size = len(prompt)
+    uncond = _encode(model, [""] * batch_size, model.bert)
+    text = _encode(model, prompt, model.bert)
+    latent, latents = init_latent(latent, model, height, width, generator, batch_size)
+    context = torch.cat([uncond, text])
+    model.scheduler.set_timesteps(num_inference_steps)
+    for t in model.scheduler.timesteps:
+        latents = diffusion_step(model, controller, latents, context, t, guidance_scale)
+    image = latent2image(model.vqvae, latents) if getattr(model, "vqvae", None) is not None else latents
+    return image, latent
+
+
+@torch.no_grad()
+def text2image_ldm_stable(model, prompt: List[str], controller, num_inference_steps: int = 50,
+                          guidance_scale: float = 7.5, generator: Optional[torch.Generator] = None,
+                          latent: Optional[torch.FloatTensor] = None, low_resource: bool = False,
+                          uncond_embeddings=None):
+    """ptp_utils.py:129-172.  ``uncond_embeddings`` (per-step list or one tensor) is the
+    argument the missing null-text notebook passes for the edit after inversion.  Without a
+    VAE on the model the final latents are returned in place of the image."""
+    register_attention_control(model, controller)
+    height = width = 512
+    batch_size = len(prompt)
+    text = _encode(model, prompt, model.text_encoder)
+    if uncond_embeddings is None:
+        uncond = _encode(model, [""] * batch_size, model.text_encoder)
+    else:
+        uncond = None
+    latent, latents = init_latent(latent, model, height, width, generator, batch_size)
+    model.scheduler.set_timesteps(num_inference_steps)
+    for i, t in enumerate(model.scheduler.timesteps):
+        if uncond_embeddings is not None:
+            u = uncond_embeddings[i] if isinstance(uncond_embeddings, (list, tuple)) else uncond_embeddings
+            uncond = u.expand(*text.shape)
+        context = [uncond, text] if low_resource else torch.cat([uncond, text])
+        latents = diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource)
+    image = latent2image(model.vae, latents) if getattr(model, "vae", None) is not None else latents
+    return image, latent
+
+
+# ------------------------------------------------------------------ the hook
+class DummyController:
+    """ptp_utils.py:212-218: identity controller (used by null-text inversion)."""
+
+    def __call__(self, *args):
+        return args[0]
+
+    def attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask=None):
+        if mask is not None:
+            return materialized_attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask)
+        return plain_attention(q, k, v, heads, scale)
+
+    def __init__(self):
+        self.num_att_layers = 0
+
+
+def _make_forward(module, place_in_unet, controller):
+    to_out = module.to_out[0] if type(module.to_out) is torch.nn.modules.container.ModuleList else module.to_out
+    attend = getattr(controller, "attention", None)
+
+    def forward(x, context=None, mask=None, encoder_hidden_states=None, attention_mask=None):
+        q = module.to_q(x)
+        is_cross = context is not None          # only the ``context=`` kwarg counts (:187)
+        src = context if is_cross else x
+        k = module.to_k(src)
+        v = module.to_v(src)
+        if attend is not None:
+            out = attend(q, k, v, module.heads, module.scale, is_cross, place_in_unet, mask)
+        else:
+            out = materialized_attention(controller, q, k, v, module.heads, module.scale, is_cross,
+                                         place_in_unet, mask)
+        return to_out(out)
+
+    return forward
+
+
+def register_attention_control(model, controller):
+    if controller is None:
+        controller = DummyController()
+
+    def walk(net, count, place):
+        if net.__class__.__name__ == "CrossAttention":
+            net.forward = _make_forward(net, place, controller)
+            return count + 1
+        if hasattr(net, "children"):
+            for child in net.children():
+                count = walk(child, count, place)
+        return count
+
+    total = 0
+    for name, net in model.unet.named_children():
+        if "down" in name:
+            total += walk(net, 0, "down")
+        elif "up" in name:
+            total += walk(net, 0, "up")
+        elif "mid" in name:
+            total += walk(net, 0, "mid")
+    controller.num_att_layers = total

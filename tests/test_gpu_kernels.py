@@ -1,0 +1,162 @@
+"""HIP kernels vs plain fp32 references (GPU).
+
+Tolerances (north star): attention probabilities within 1e-5 max-abs in the exact-f32 check
+mode and 2e-3 at bf16; outputs O = P V are checked relative to max|V|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from p2p_amd import _hip
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_probs(q, k, heads, scale, qk_src=None):
+    N, P, C = q.shape
+    d = C // heads
+    if qk_src is not None:
+        q, k = q[qk_src], k[qk_src]
+    qh = q.float().reshape(N, P, heads, d).permute(0, 2, 1, 3)
+    kh = k.float().reshape(N, k.shape[1], heads, d).permute(0, 2, 1, 3)
+    return (torch.einsum("nhid,nhjd->nhij", qh, kh) * scale).softmax(-1)      # [N, H, P, K]
+
+
+def ref_out(probs, v, heads):
+    N, K, C = v.shape
+    vh = v.float().reshape(N, K, heads, C // heads).permute(0, 2, 1, 3)
+    o = torch.einsum("nhij,nhjd->nhid", probs, vh)
+    return o.permute(0, 2, 1, 3).reshape(N, probs.shape[2], C)
+
+
+def make_qkv(N, P, K, heads, d, dtype, qscale=1.0, seed=0, dev="cuda"):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    C = heads * d
+    q = (torch.randn(N, P, C, device=dev, generator=g) * qscale).to(dtype)
+    k = torch.randn(N, K, C, device=dev, generator=g).to(dtype)
+    v = torch.randn(N, K, C, device=dev, generator=g).to(dtype)
+    return q, k, v
+
+
+SELF_GEOMS = [  # (N, P, K, heads, d)
+    (2, 4096, 4096, 2, 40), (2, 1024, 1024, 2, 80), (4, 256, 256, 8, 160), (4, 64, 64, 8, 160),
+    (2, 100, 77, 2, 64), (2, 200, 130, 4, 16), (3, 33, 96, 2, 8),
+]
+
+
+@pytest.mark.parametrize("geom", SELF_GEOMS, ids=lambda g: "x".join(map(str, g)))
+@pytest.mark.parametrize("compute", ["f32", "bf16"])
+def test_self_attention_output(cuda, geom, compute):
+    N, P, K, H, d = geom
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32)
+    o = torch.empty_like(q)
+    scale = d ** -0.5
+    _hip.self_attn(q, k, v, o, H, scale, compute=compute)
+    torch.cuda.synchronize()
+    want = ref_out(ref_probs(q, k, H, scale), v, H)
+    err = (o - want).abs().max().item()
+    tol = 2e-5 if compute == "f32" else 2e-2
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("compute,qscale,tol", [("f32", 1.0, 1e-5), ("f32", 12.0, 1e-5),
+                                               ("bf16", 1.0, 2e-3), ("bf16", 8.0, 2e-3)])
+@pytest.mark.parametrize("geom", [(2, 1024, 1024, 2, 80), (2, 256, 256, 4, 160), (2, 64, 4096, 2, 40)],
+                         ids=lambda g: "x".join(map(str, g)))
+def test_self_attention_store_probs(cuda, geom, compute, qscale, tol):
+    """The AttentionStore epilogue writes exact probabilities (two-pass mode)."""
+    N, P, K, H, d = geom
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=qscale, seed=3)
+    o = torch.empty_like(q)
+    scale = d ** -0.5
+    store = torch.full((N * H, P, K), 7.0, device=cuda)
+    slots = [n * H for n in range(N)]
+    _hip.self_attn(q, k, v, o, H, scale, compute=compute, store=store, store_slot=slots, accumulate=False)
+    p = ref_probs(q, k, H, scale)
+    err = (store - p.reshape(N * H, P, K)).abs().max().item()
+    assert err < tol, err
+    # second call accumulates (running sum of AttentionStore.between_steps)
+    _hip.self_attn(q, k, v, o, H, scale, compute=compute, store=store, store_slot=slots, accumulate=True)
+    err2 = (store - 2 * p.reshape(N * H, P, K)).abs().max().item()
+    assert err2 < 2 * tol, err2
+    want = ref_out(p, v, H)
+    assert (o - want).abs().max().item() < (2e-5 if compute == "f32" else 2e-2)
+
+
+def test_self_attention_injection_and_partial_store(cuda):
+    N, P, K, H, d = 8, 256, 256, 8, 160
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, seed=5)
+    o = torch.empty_like(q)
+    scale = d ** -0.5
+    src = [0, 1, 2, 3, 4, 4, 4, 4]           # cond edits read the cond source's P (main.py:171)
+    store = torch.zeros(4 * H, P, K, device=cuda)
+    slots = [-1, -1, -1, -1, 0, H, 2 * H, 3 * H]
+    _hip.self_attn(q, k, v, o, H, scale, compute="f32", qk_src=src, store=store, store_slot=slots)
+    p = ref_probs(q, k, H, scale, qk_src=src)
+    assert (o - ref_out(p, v, H)).abs().max().item() < 2e-5
+    assert (store - p[4:].reshape(4 * H, P, K)).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("io", [torch.bfloat16])
+def test_self_attention_bf16_io(cuda, io):
+    N, P, K, H, d = 2, 1024, 1024, 8, 80
+    q, k, v = make_qkv(N, P, K, H, d, io, seed=9)
+    o = torch.empty_like(q)
+    _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16")
+    want = ref_out(ref_probs(q, k, H, d ** -0.5), v, H)
+    assert o.dtype == io
+    assert (o.float() - want).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
+@pytest.mark.parametrize("geom", [(4, 4096, 77, 8, 40), (4, 256, 77, 8, 160), (6, 100, 77, 2, 16)],
+                         ids=lambda g: "x".join(map(str, g)))
+def test_probs_and_pv_materialise(cuda, geom, compute, tol):
+    N, P, K, H, d = geom
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=4.0, seed=11)
+    scale = d ** -0.5
+    probs = torch.empty(N * H, P, K, device=cuda)
+    _hip.attn_probs(q, k, H, scale, probs, compute=compute)
+    p = ref_probs(q, k, H, scale)
+    assert (probs - p.reshape(N * H, P, K)).abs().max().item() < tol
+    o = torch.empty_like(q)
+    _hip.attn_pv(probs, v, o, H, compute=compute)
+    want = ref_out(probs.reshape(N, H, P, K), v, H)
+    assert (o - want).abs().max().item() < (1e-5 if compute == "f32" else 2e-2)
+
+
+@pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
+def test_cross_plain_groups(cuda, compute, tol):
+    N, P, K, H, d = 8, 1024, 77, 8, 80
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=6.0, seed=13)
+    scale = d ** -0.5
+    o = torch.empty_like(q)
+    store = torch.zeros(N * H, P, K, device=cuda)
+    groups = [(n, 1, None, None) for n in range(N)]
+    _hip.cross_attn(q, k, v, o, H, scale, groups, compute=compute, store=store,
+                    store_slot=[n * H for n in range(N)])
+    p = ref_probs(q, k, H, scale)
+    assert (store - p.reshape(N * H, P, K)).abs().max().item() < tol
+    assert (o - ref_out(p, v, H)).abs().max().item() < (2e-5 if compute == "f32" else 2e-2)
+
+
+def test_key_mask_materialise(cuda):
+    N, P, K, H, d = 2, 64, 77, 2, 16
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, seed=17)
+    mask = torch.ones(N, K, dtype=torch.bool, device=cuda)
+    mask[0, 50:] = False
+    mask[1, :10] = False
+    probs = torch.empty(N * H, P, K, device=cuda)
+    _hip.attn_probs(q, k, H, d ** -0.5, probs, compute="f32", key_mask=mask.to(torch.uint8))
+    # ptp_utils.py:197-201: rows (n*H + h) take mask row (n*H + h) % N (head-major repeat)
+    sim = torch.einsum("nhid,nhjd->nhij", q.reshape(N, P, H, d).permute(0, 2, 1, 3),
+                       k.reshape(N, K, H, d).permute(0, 2, 1, 3)).reshape(N * H, P, K) * d ** -0.5
+    m = mask[:, None, :].repeat(H, 1, 1)
+    sim.masked_fill_(~m, -torch.finfo(sim.dtype).max)
+    assert (probs - sim.softmax(-1)).abs().max().item() < 1e-5
+
+
+def test_store_scale(cuda):
+    x = torch.randn(3, 1000, 77, device=cuda)
+    y = _hip.store_scale(x, 7.0)
+    assert torch.equal(y, x / 7)

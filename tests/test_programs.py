@@ -1,0 +1,140 @@
+"""Device edit programs (host side): decode the blob exactly as the cross kernel reads it and
+check the result against the oracle's materialised edit (main.py:180-197 semantics)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import control as oc
+from oracle import tables as otab
+from p2p_amd import controllers as pc
+from p2p_amd import null_text as pn
+from p2p_amd import programs
+
+COLS = programs.PROGRAM_COLS
+
+
+def run_blob(blob: np.ndarray, P0: np.ndarray, Pb: np.ndarray, alpha: np.ndarray) -> np.ndarray:
+    """Reference interpreter of the kernel's edit step (p2p_attn.hip cross_attn_kernel)."""
+    hdr = blob[:16].view(np.int32)
+    E, n, nnz = int(hdr[0]), int(hdr[1]), int(hdr[2])
+    off = 16
+    crep = blob[off:off + 4 * E * COLS].view(np.float32).reshape(E, COLS); off += 4 * E * COLS
+    post = blob[off:off + 4 * E * COLS].view(np.float32).reshape(E, COLS); off += 4 * E * COLS
+    colptr = blob[off:off + 4 * E * COLS].view(np.int32).reshape(E, COLS); off += 4 * E * COLS
+    rowidx = blob[off:off + 4 * nnz].view(np.int32); off += 4 * nnz
+    val = blob[off:off + 4 * nnz].view(np.float32)
+    out = Pb.copy()                                   # [E, H, P, n]
+    for e in range(E):
+        for w in range(n):
+            pb = Pb[e, ..., w]
+            acc = (crep[e, w] * pb).astype(np.float32)
+            for t in range(colptr[e, w], colptr[e, w + 1]):
+                acc = (acc + np.float32(val[t]) * P0[..., rowidx[t]]).astype(np.float32)
+            R = (post[e, w] * acc).astype(np.float32)
+            a = np.float32(alpha[e, w])
+            out[e, ..., w] = (a * R + (np.float32(1) - a) * pb).astype(np.float32)
+    return out
+
+
+def rand_probs(shape, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * 3).softmax(-1)
+
+
+PROMPTS_R = ["a painting of a squirrel eating a burger", "a painting of a lion eating a burger",
+             "a painting of a cat eating a burger", "a painting of a squirrel eating a lasagna"]
+PROMPTS_F = ["a cat eating a burger", "a fluffy cat eating a burger", "a cat eating a burger at night"]
+
+
+def _check(ctrl, oracle, step, tok, exact=True):
+    E = ctrl.batch_size - 1
+    H, P = 2, 8
+    base = rand_probs((H, P, 77), 1)
+    rep = rand_probs((E, H, P, 77), 2)
+    alpha = ctrl.cross_replace_alpha[step].reshape(E, 77).numpy()
+    got = run_blob(ctrl._edit_program().blob(), base.numpy(), rep.numpy(), alpha)
+    a = oracle.alpha[step]
+    want = (oracle.cross_edit(base, rep) * a + (1 - a) * rep).reshape(E, H, P, 77).numpy()
+    if exact:
+        assert np.array_equal(got, want)
+    else:
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("step", [0, 30, 45])
+def test_replace_program(tok, step):
+    ctrl = pc.AttentionReplace(PROMPTS_R, 50, {"default_": .8, "lasagna": .2}, .4, tokenizer=tok, device="cpu")
+    orc = oc.OracleController("main", "replace", PROMPTS_R, 50, {"default_": .8, "lasagna": .2}, .4, tok)
+    _check(ctrl, orc, step, tok)
+
+
+def test_replace_program_multitoken(tok):
+    prompts = ["a beautiful mountain landscape", "a colorful mountain landscape", "pizza mountain landscape"]
+    with pytest.raises(ValueError):
+        pc.AttentionReplace(prompts, 10, .8, .4, tokenizer=tok, device="cpu")
+    prompts = ["a beautiful mountain landscape", "a colorful mountain landscape"]
+    ctrl = pc.AttentionReplace(prompts, 10, .8, .4, tokenizer=tok, device="cpu")
+    orc = oc.OracleController("main", "replace", prompts, 10, .8, .4, tok)
+    _check(ctrl, orc, 0, tok, exact=False)   # 3 source tokens summed per column: order may differ
+
+
+@pytest.mark.parametrize("step", [0, 40])
+def test_refine_program(tok, step):
+    ctrl = pc.AttentionRefine(PROMPTS_F, 50, .8, .4, tokenizer=tok, device="cpu")
+    orc = oc.OracleController("main", "refine", PROMPTS_F, 50, .8, .4, tok)
+    _check(ctrl, orc, step, tok)
+
+
+def test_reweight_programs(tok):
+    eq = pc.get_equalizer(PROMPTS_F[1], "fluffy", (2.5,), tokenizer=tok)
+    ctrl = pc.AttentionReweight(PROMPTS_F, 50, .8, .4, equalizer=eq, tokenizer=tok, device="cpu")
+    orc = oc.OracleController("main", "reweight", PROMPTS_F, 50, .8, .4, tok, equalizer=eq)
+    _check(ctrl, orc, 0, tok)
+    eqn = pn.get_equalizer(PROMPTS_R[3], ("lasagna", "squirrel"), (3.0, .5), tokenizer=tok)
+    inner = pn.AttentionReplace(PROMPTS_R, 50, .8, .4, tokenizer=tok, device="cpu")
+    ctrl = pn.AttentionReweight(PROMPTS_R, 50, .8, .4, equalizer=eqn, controller=inner, tokenizer=tok, device="cpu")
+    oinner = oc.OracleController("null", "replace", PROMPTS_R, 50, .8, .4, tok)
+    orc = oc.OracleController("null", "reweight", PROMPTS_R, 50, .8, .4, tok, equalizer=eqn, inner=oinner)
+    _check(ctrl, orc, 0, tok)
+    inner = pn.AttentionRefine(PROMPTS_F, 50, .8, .4, tokenizer=tok, device="cpu")
+    eqf = pn.get_equalizer(PROMPTS_F[1], ("fluffy",), (4.0,), tokenizer=tok)
+    ctrl = pn.AttentionReweight(PROMPTS_F, 50, .8, .4, equalizer=eqf, controller=inner, tokenizer=tok, device="cpu")
+    oinner = oc.OracleController("null", "refine", PROMPTS_F, 50, .8, .4, tok)
+    orc = oc.OracleController("null", "reweight", PROMPTS_F, 50, .8, .4, tok, equalizer=eqf, inner=oinner)
+    _check(ctrl, orc, 0, tok)
+
+
+def test_fused_support_detection(tok):
+    r = pc.AttentionReplace(PROMPTS_R, 50, .8, .4, tokenizer=tok, device="cpu")
+    assert r.fused_supported()
+
+    class Custom(pc.AttentionReplace):
+        def replace_cross_attention(self, a, b):
+            return super().replace_cross_attention(a, b) * 2
+
+    assert not Custom(PROMPTS_R, 50, .8, .4, tokenizer=tok, device="cpu").fused_supported()
+
+    class Blend(pn.AttentionRefine):
+        def step_callback(self, x_t):   # free to override: not encoded in the kernel
+            return x_t
+
+    assert Blend(PROMPTS_F, 50, .8, .4, tokenizer=tok, device="cpu").fused_supported()
+
+    class Inner(pc.AttentionReplace):
+        def replace_cross_attention(self, a, b):
+            return a
+    eq = pc.get_equalizer(PROMPTS_R[1], "lion", (2.0,), tokenizer=tok)
+    rw = pc.AttentionReweight(PROMPTS_R, 50, .8, .4, equalizer=eq,
+                              controller=Inner(PROMPTS_R, 50, .8, .4, tokenizer=tok, device="cpu"),
+                              tokenizer=tok, device="cpu")
+    with pytest.raises(pc.NotFusable):
+        rw._edit_program()
+
+
+def test_program_blob_layout():
+    m = torch.zeros(2, 77, 77)
+    m[:, torch.arange(77), torch.arange(77)] = 1
+    blob = programs.replace_program(m).blob()
+    hdr = blob[:16].view(np.int32)
+    assert hdr.tolist() == [2, 77, 154, COLS]
+    assert blob.nbytes == 16 + 3 * 4 * 2 * COLS + 8 * 154
