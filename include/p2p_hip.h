@@ -124,7 +124,9 @@ typedef struct {
 
 int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream);
 
-/* AttentionStore.get_average_attention (main.py:144-149): dst = src / divisor. */
+/* AttentionStore.get_average_attention (main.py:144-149): dst = src / divisor, computed as
+ * src * (1.0f / divisor) -- what torch does for `cuda_tensor / python_scalar` on the
+ * reference's cuda:0 device. */
 int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream);
 
 /* Build/runtime information. */

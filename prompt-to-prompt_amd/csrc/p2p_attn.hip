@@ -22,26 +22,30 @@ namespace p2p {
 // MODE_PV    : O = P V with P read from HBM                                     (materialise)
 enum { MODE_FUSED = 0, MODE_STORE = 1, MODE_PROBS = 2, MODE_PV = 3 };
 
-template <typename IO, typename M, int D, int BK, int WAVES, int MODE>
+template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, int MODE>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
-  using E = typename M::elem;
+  using EK = typename MQ::elem;
+  using EV = typename MP::elem;
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   constexpr int NKT = DK / 16;
   constexpr int NDT = DV / 32;
   constexpr int NSB = BK / 32;
-  constexpr int KS = KStride<DK, M::kElemBytes>::value;
-  constexpr int VS = (M::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
+  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
+  constexpr int VS = (MP::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
   constexpr int NT = 64 * WAVES;
   constexpr int CPR = D / 8;
   constexpr int NCH = (BK * CPR + NT - 1) / NT;
   constexpr bool kNeedK = MODE != MODE_PV;
   constexpr bool kNeedV = MODE == MODE_FUSED || MODE == MODE_STORE || MODE == MODE_PV;
-  constexpr int KBUF = kNeedK ? 2 * BK * KS : 0;
-  constexpr int VBUF = kNeedV ? 2 * BK * VS : 0;
-  __shared__ __attribute__((aligned(16))) E smem[KBUF + VBUF + 8];
-  E* const Ks = smem;
-  E* const Vs = smem + KBUF;
+  constexpr int KPLANE = BK * KS;                       // elements per K plane
+  constexpr int KBUF = kNeedK ? KPLANE * MQ::planes : 0;  // elements per K buffer
+  constexpr int VBUF = kNeedV ? BK * VS : 0;
+  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
+  constexpr int VBYTES = 2 * VBUF * (int)sizeof(EV);
+  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
+  EK* const Ks = reinterpret_cast<EK*>(smem);
+  EV* const Vs = reinterpret_cast<EV*>(smem + KBYTES);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -66,21 +70,15 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
   IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
 
   // zero the LDS image once: pad columns [D, DK) / [D, DV) and rows >= K stay zero.
-  for (int i = tid; i < KBUF + VBUF; i += NT) smem[i] = E(0);
+  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
 
   // Q fragments stay in registers for the whole key loop.
-  typename M::frag qf[NKT];
+  typename MQ::frag qf[NKT];
   if constexpr (kNeedK) {
 #pragma unroll
     for (int t = 0; t < NKT; ++t) {
       const int col = 16 * t + 8 * hh;
-      if (prow && col < D) {
-        E tmp[8] __attribute__((aligned(16)));
-        load8_global<IO, M>(qp + (int64_t)p * a.ldq + col, tmp);
-        qf[t] = M::load8(tmp);
-      } else {
-        qf[t] = M::zero();
-      }
+      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
     }
   }
 
@@ -108,22 +106,22 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
       if (cidx < BK * CPR) {
         const int row = cidx / CPR;
         const int ch = cidx - row * CPR;
-        if (withK) kreg[i].store(Ks + buf * BK * KS + row * KS + ch * 8);
-        if (withV) vreg[i].store(Vs + buf * BK * VS + row * VS + ch * 8);
+        if (withK) MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
+        if (withV) vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
       }
     }
   };
 
   // S^T block sb of the tile in buffer buf, masked beyond K (and by the optional key mask).
   auto scores = [&](int buf, int kt, float (&sv)[NSB][16]) {
-    const E* Kb = Ks + buf * BK * KS;
+    const EK* Kb = Ks + buf * KBUF;
 #pragma unroll
     for (int sb = 0; sb < NSB; ++sb) {
       f32x16_t acc = {};
 #pragma unroll
       for (int t = 0; t < NKT; ++t) {
-        const typename M::frag fa = M::load8(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh);
-        M::mma(acc, fa, qf[t]);
+        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+        MQ::mma(acc, fa, qf[t]);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
@@ -181,9 +179,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
-      const E* Vb = Vs + buf * BK * VS;
+      const EV* Vb = Vs + buf * VBUF;
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(M{}, O, Vb, sb * 32, sv[sb], lane);
+      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
       if (kt + 1 < ntiles) stage_write(buf ^ 1, true, true);
       __syncthreads();
     }
@@ -265,9 +263,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
           }
       }
       if constexpr (kPV) {
-        const E* Vb = Vs + buf * BK * VS;
+        const EV* Vb = Vs + buf * VBUF;
 #pragma unroll
-        for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(M{}, O, Vb, sb * 32, sv[sb], lane);
+        for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
       }
       if (kt + 1 < ntiles) stage_write(buf ^ 1, true, kPV);
       __syncthreads();
@@ -289,9 +287,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
           const int key = kt * BK + sb * 32 + acc_row(r, hh);
           sv[sb][r] = (prow && key < K) ? pp[key] : 0.f;
         }
-      const E* Vb = Vs + buf * BK * VS;
+      const EV* Vb = Vs + buf * VBUF;
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(M{}, O, Vb, sb * 32, sv[sb], lane);
+      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
       if (kt + 1 < ntiles) stage_write(buf ^ 1, false, true);
       __syncthreads();
     }
@@ -313,35 +311,40 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
 }
 
 // ====================================================================== cross attention
-// One workgroup = one head x one tile of 32*WAVES queries x one prompt group.  The group's
-// prompts are processed in order; the source prompt's probabilities P0 are parked in LDS
-// (one 32-row slab per wave) so each edit can gather from them:
+// One workgroup = one head x one tile of 32*WAVES queries x one batch entry n.  An edit entry
+// (position b > 0 of a prompt group that carries an edit program) first recomputes the
+// source prompt's probabilities P0 for the same rows (the K = 77 cross product is cheap) and
+// parks them in LDS, one 32-row slab per wave, so the edit can gather from them:
 //   R[w]  = post[w] * ( c_rep[w] * P_b[w] + sum_t val[t] * P0[rowidx[t]] ),  t in column w
 //   P_b'  = alpha[w] * R[w] + (1 - alpha[w]) * P_b[w]
 // which is AttentionReplace (c_rep 0, mapper column w), AttentionRefine (c_rep 1-a, one term
 // mapper[w] with weight a), AttentionReweight (c_rep 0, term (w, eq[w])), and Reweight
-// chained on either (post = eq) -- host side: p2p_amd/programs.py.
-template <typename IO, typename M, int D, int WAVES>
+// chained on either (post = eq) -- host side: p2p_amd/programs.py.  Stored maps leave through
+// the same LDS slab as whole contiguous rows (one [32, K] block per wave).
+template <typename IO, typename MQ, typename MP, int D, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
-  using E = typename M::elem;
+  using EK = typename MQ::elem;
+  using EV = typename MP::elem;
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   constexpr int NKT = DK / 16;
   constexpr int NDT = DV / 32;
   constexpr int KB = P2P_MAX_KEYS_CROSS / 32;
   constexpr int KR = KB * 32;
-  constexpr int KS = KStride<DK, M::kElemBytes>::value;
-  constexpr int VS = (M::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
+  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
+  constexpr int VS = (MP::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
   constexpr int NT = 64 * WAVES;
   constexpr int CPR = D / 8;
+  constexpr int NCH = (KR * CPR + NT - 1) / NT;
   constexpr int P0S = KR + 1;  // odd f32 stride: 32 rows reading one column hit 32 banks
-  constexpr int KBYTES = KR * KS * (int)sizeof(E);
-  constexpr int VBYTES = KR * VS * (int)sizeof(E);
+  constexpr int KPLANE = KR * KS;
+  constexpr int KBYTES = KPLANE * MQ::planes * (int)sizeof(EK);
+  constexpr int VBYTES = KR * VS * (int)sizeof(EV);
   constexpr int PBYTES = WAVES * 32 * P0S * 4;
   __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + PBYTES];
-  E* const Ks = reinterpret_cast<E*>(smem);
-  E* const Vs = reinterpret_cast<E*>(smem + KBYTES);
-  float* const P0 = reinterpret_cast<float*>(smem + KBYTES + VBYTES);
+  EK* const Ks = reinterpret_cast<EK*>(smem);
+  EV* const Vs = reinterpret_cast<EV*>(smem + KBYTES);
+  float* const slab = reinterpret_cast<float*>(smem + KBYTES + VBYTES) + (threadIdx.x >> 6) * 32 * P0S;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -353,77 +356,63 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
   const int qt = logical % a.n_qtiles;
   const int rest = logical / a.n_qtiles;
   const int h = rest % a.H;
-  const int gi = rest / a.H;
+  const int n = rest / a.H;
+  const int gi = a.ent_group[n];
   const int first = a.grp_first[gi];
-  const int count = a.grp_count[gi];
+  const int b = n - first;
   const char* const prog = static_cast<const char*>(a.grp_prog[gi]);
-  const float* const alpha = a.grp_alpha[gi];
-  const int p = qt * 32 * WAVES + wave * 32 + qi;
+  const bool edit = prog != nullptr && b > 0;
+  const int p0w = qt * 32 * WAVES + wave * 32;
+  const int p = p0w + qi;
   const bool prow = p < a.P;
   const int K = a.K;
   const float c = a.scale_log2;
-  float* const P0w = P0 + wave * 32 * P0S + qi * P0S;
 
   for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
+  __syncthreads();
 
-  // edit program tables (P2P_PROGRAM_COLS-strided; see p2p_amd/programs.py)
-  int n_edits = 0, nnz = 0;
-  const float* crep = nullptr;
-  const float* post = nullptr;
-  const int* colptr = nullptr;
-  const int* rowidx = nullptr;
-  const float* val = nullptr;
-  if (prog) {
-    const int* hdr = reinterpret_cast<const int*>(prog);
-    n_edits = hdr[0];
-    nnz = hdr[2];
-    crep = reinterpret_cast<const float*>(prog + 16);
-    post = crep + n_edits * P2P_PROGRAM_COLS;
-    colptr = reinterpret_cast<const int*>(post + n_edits * P2P_PROGRAM_COLS);
-    rowidx = colptr + n_edits * P2P_PROGRAM_COLS;
-    val = reinterpret_cast<const float*>(rowidx + nnz);
-  }
-
-  for (int b = 0; b < count; ++b) {
-    const int n = first + b;
-    const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)n * a.bsq + h * D;
-    const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)n * a.bsk + h * D;
-    const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
-    IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
-
-    __syncthreads();  // previous prompt's LDS reads are done
-    for (int cidx = tid; cidx < K * CPR; cidx += NT) {
+  auto stage = [&](int e, bool withV) {
+    const IO* kp = static_cast<const IO*>(a.k) + (int64_t)e * a.bsk + h * D;
+    const IO* vp = static_cast<const IO*>(a.v) + (int64_t)e * a.bsv + h * D;
+    Chunk8<IO> kc[NCH], vc[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
-      Chunk8<IO> kc, vc;
-      kc.load(kp + (int64_t)row * a.ldk + ch * 8);
-      vc.load(vp + (int64_t)row * a.ldv + ch * 8);
-      kc.store(Ks + row * KS + ch * 8);
-      vc.store(Vs + row * VS + ch * 8);
+      if (cidx < KR * CPR && row < K) {
+        kc[i].load(kp + (int64_t)row * a.ldk + ch * 8);
+        if (withV) vc[i].load(vp + (int64_t)row * a.ldv + ch * 8);
+      }
     }
-    typename M::frag qf[NKT];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      const int row = cidx / CPR;
+      const int ch = cidx - row * CPR;
+      if (cidx < KR * CPR && row < K) {
+        MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
+        if (withV) vc[i].store(Vs + row * VS + ch * 8);
+      }
+    }
+  };
+
+  // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row
+  auto probs = [&](int e, float (&sv)[KB][16]) {
+    const IO* qp = static_cast<const IO*>(a.q) + (int64_t)e * a.bsq + h * D;
+    typename MQ::frag qf[NKT];
 #pragma unroll
     for (int t = 0; t < NKT; ++t) {
       const int col = 16 * t + 8 * hh;
-      if (prow && col < D) {
-        E tmp[8] __attribute__((aligned(16)));
-        load8_global<IO, M>(qp + (int64_t)p * a.ldq + col, tmp);
-        qf[t] = M::load8(tmp);
-      } else {
-        qf[t] = M::zero();
-      }
+      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
     }
-    __syncthreads();
-
-    // ---- S^T and the exact softmax over the K keys
-    float sv[KB][16];
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
       f32x16_t acc = {};
 #pragma unroll
       for (int t = 0; t < NKT; ++t) {
-        const typename M::frag fa = M::load8(Ks + (kb * 32 + qi) * KS + 16 * t + 8 * hh);
-        M::mma(acc, fa, qf[t]);
+        const typename MQ::frag fa = MQ::load_k(Ks + (kb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+        MQ::mma(acc, fa, qf[t]);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[kb][r] = (kb * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
@@ -439,163 +428,189 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = fast_exp2(fmaf(sv[kb][r], c, -mx));
-        sv[kb][r] = e;
-        ls += e;
+        const float ex = fast_exp2(fmaf(sv[kb][r], c, -mx));
+        sv[kb][r] = ex;
+        ls += ex;
       }
     const float inv = 1.f / (ls + __shfl_xor(ls, 32));
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[kb][r] *= inv;
+  };
 
-    // ---- P2P cross edit (cond groups only)
-    if (prog && count > 1) {
-      if (b == 0) {
+  float sv[KB][16];
+  if (edit) {
+    // ---- source probabilities P0 for these rows -> this wave's LDS slab
+    stage(first, false);
+    __syncthreads();
+    probs(first, sv);
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int w = kb * 32 + acc_row(r, hh);
-            if (w < K) P0w[w] = sv[kb][r];
-          }
-        __syncthreads();
-      } else {
-        const int e = b - 1;
-        const float* ce = crep + e * P2P_PROGRAM_COLS;
-        const float* pe = post + e * P2P_PROGRAM_COLS;
-        const int* cp = colptr + e * P2P_PROGRAM_COLS;
-        const float* al = alpha + e * K;
+      for (int r = 0; r < 16; ++r) {
+        const int w = kb * 32 + acc_row(r, hh);
+        if (w < K) slab[qi * P0S + w] = sv[kb][r];
+      }
+    __syncthreads();  // slab written; every wave is done reading the source K tile
+  }
+  stage(n, true);
+  __syncthreads();
+  probs(n, sv);
+
+  if (edit) {
+    const int* hdr = reinterpret_cast<const int*>(prog);
+    const int n_edits = hdr[0];
+    const int nnz = hdr[2];
+    const float* crep = reinterpret_cast<const float*>(prog + 16);
+    const float* post = crep + n_edits * P2P_PROGRAM_COLS;
+    const int* colptr = reinterpret_cast<const int*>(post + n_edits * P2P_PROGRAM_COLS);
+    const int* rowidx = colptr + n_edits * P2P_PROGRAM_COLS;
+    const float* val = reinterpret_cast<const float*>(rowidx + nnz);
+    const int e = b - 1;
+    const float* ce = crep + e * P2P_PROGRAM_COLS;
+    const float* pe = post + e * P2P_PROGRAM_COLS;
+    const int* cp = colptr + e * P2P_PROGRAM_COLS;
+    const float* al = a.grp_alpha[gi] + e * K;
+    const float* P0 = slab + qi * P0S;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int w = kb * 32 + acc_row(r, hh);
-            if (w < K) {
+      for (int r = 0; r < 16; ++r) {
+        const int w = kb * 32 + acc_row(r, hh);
+        if (w < K) {
 #pragma clang fp contract(off)
-              const float pb = sv[kb][r];
-              float acc = ce[w] * pb;
-              const int t1 = cp[w + 1];
-              for (int t = cp[w]; t < t1; ++t) acc = acc + val[t] * P0w[rowidx[t]];
-              const float R = pe[w] * acc;
-              const float aw = al[w];
-              sv[kb][r] = aw * R + (1.f - aw) * pb;
-            }
-          }
+          const float pb = sv[kb][r];
+          float acc = ce[w] * pb;
+          const int t1 = cp[w + 1];
+          for (int t = cp[w]; t < t1; ++t) acc = acc + val[t] * P0[rowidx[t]];
+          const float R = pe[w] * acc;
+          const float aw = al[w];
+          sv[kb][r] = aw * R + (1.f - aw) * pb;
+        }
+      }
+  }
+
+  // ---- AttentionStore epilogue: post-edit maps, whole rows through the wave's slab
+  const int slot = a.store_slot[n];
+  if (a.store && slot >= 0) {
+    __syncthreads();  // every lane of the wave is done gathering from the slab
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int w = kb * 32 + acc_row(r, hh);
+        if (w < K) slab[qi * K + w] = sv[kb][r];
+      }
+    __syncthreads();
+    const int rows = min(32, a.P - p0w);
+    if (rows > 0) {
+      float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
+      const int count = rows * K;
+      if (((uintptr_t)g & 15) == 0 && (count & 3) == 0) {
+        for (int i = lane; i < count / 4; i += 64) {
+          f32x4_t v = reinterpret_cast<const f32x4_t*>(slab)[i];
+          f32x4_t* dst = reinterpret_cast<f32x4_t*>(g) + i;
+          if (a.store_accumulate) v += *dst;
+          *dst = v;
+        }
+      } else {
+        for (int i = lane; i < count; i += 64) g[i] = a.store_accumulate ? g[i] + slab[i] : slab[i];
       }
     }
+  }
 
-    // ---- AttentionStore epilogue (post-edit maps)
-    const int slot = a.store_slot[n];
-    if (a.store && slot >= 0 && prow) {
-      float* mp = a.store + ((int64_t)(slot + h) * a.P + p) * (int64_t)K;
+  // ---- O = P' V
+  f32x16_t O[NDT];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int w = kb * 32 + acc_row(r, hh);
-          if (w < K) mp[w] = a.store_accumulate ? mp[w] + sv[kb][r] : sv[kb][r];
-        }
-    }
-
-    // ---- O = P' V
-    f32x16_t O[NDT];
+  for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
+  if (prow) {
+    IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(M{}, O, Vs, kb * 32, sv[kb], lane);
-    if (prow) {
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int dd = dt * 32 + 8 * g + 4 * hh;
-          if (dd < D)
-            store4(op + (int64_t)p * a.ldo + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2],
-                   O[dt][4 * g + 3]);
-        }
-    }
+      for (int g = 0; g < 4; ++g) {
+        const int dd = dt * 32 + 8 * g + 4 * hh;
+        if (dd < D)
+          store4(op + (int64_t)p * a.ldo + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2],
+                 O[dt][4 * g + 3]);
+      }
   }
 }
 
 // ====================================================================== launchers
-template <typename IO, typename M, int D>
+template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
-  constexpr int BK = (D >= 128 || M::kElemBytes == 4) ? 32 : 64;
-  const bool small = a.P <= 64;
+  constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
   SelfArgs b = a;
-  if (small) {
-    constexpr int W = 2;
-    b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
-    dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-    switch (mode) {
-      case MODE_FUSED: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_FUSED>), grid, block, 0, st, b); break;
-      case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break;
-      case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break;
-      default: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;
-    }
-  } else {
-    constexpr int W = 4;
-    b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
-    dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-    switch (mode) {
-      case MODE_FUSED: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_FUSED>), grid, block, 0, st, b); break;
-      case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break;
-      case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break;
-      default: hipLaunchKernelGGL((self_attn_kernel<IO, M, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;
-    }
+#define P2P_LAUNCH_SELF(W)                                                                                   \
+  {                                                                                                          \
+    b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);                                                              \
+    dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);                                                        \
+    switch (mode) {                                                                                          \
+      case MODE_FUSED: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_FUSED>), grid, block, 0, st, b); break; \
+      case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break; \
+      case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break; \
+      default: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;         \
+    }                                                                                                        \
   }
+  if (a.P <= 64) P2P_LAUNCH_SELF(2) else P2P_LAUNCH_SELF(4)
+#undef P2P_LAUNCH_SELF
   return hipGetLastError();
 }
 
-template <typename IO, typename M, int D>
-static hipError_t launch_cross_d(const CrossArgs& a, int n_groups, hipStream_t st) {
-  constexpr int W = (M::kElemBytes == 4 && D >= 128) ? 2 : 4;
+template <typename IO, typename MQ, typename MP, int D>
+static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
+  constexpr int W = (MP::kElemBytes == 4 && D >= 128) ? 2 : 4;
   CrossArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
-  dim3 grid(b.n_qtiles * a.H * n_groups), block(64 * W);
-  hipLaunchKernelGGL((cross_attn_kernel<IO, M, D, W>), grid, block, 0, st, b);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
 #define P2P_FOR_EACH_D(X) X(8) X(16) X(32) X(40) X(64) X(80) X(128) X(160)
 
-template <typename IO, typename M>
+template <typename IO, typename MQ, typename MP>
 static int dispatch_self(const SelfArgs& a, int d, int mode, hipStream_t st) {
   switch (d) {
-#define P2P_CASE(DD) case DD: return (int)launch_self_d<IO, M, DD>(a, mode, st);
+#define P2P_CASE(DD) case DD: return (int)launch_self_d<IO, MQ, MP, DD>(a, mode, st);
     P2P_FOR_EACH_D(P2P_CASE)
 #undef P2P_CASE
     default: return P2P_E_HEAD_DIM;
   }
 }
 
-template <typename IO, typename M>
-static int dispatch_cross(const CrossArgs& a, int d, int n_groups, hipStream_t st) {
+template <typename IO, typename MQ, typename MP>
+static int dispatch_cross(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
-#define P2P_CASE(DD) case DD: return (int)launch_cross_d<IO, M, DD>(a, n_groups, st);
+#define P2P_CASE(DD) case DD: return (int)launch_cross_d<IO, MQ, MP, DD>(a, st);
     P2P_FOR_EACH_D(P2P_CASE)
 #undef P2P_CASE
     default: return P2P_E_HEAD_DIM;
   }
 }
 
+// Precision selection: exact-f32 check mode; bf16 pipe on f32 inputs (split-bf16 QK^T so the
+// logits keep f32 grade, bf16 PV); bf16 inputs (one bf16 MFMA per step, exact products).
 int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st) {
   if (compute == P2P_COMPUTE_F32) {
     if (io_dtype != P2P_DTYPE_F32) return P2P_E_DTYPE;
-    return dispatch_self<float, MmaF32>(a, d, mode, st);
+    return dispatch_self<float, QkF32, MmaF32>(a, d, mode, st);
   }
-  if (io_dtype == P2P_DTYPE_F32) return dispatch_self<float, MmaBf16>(a, d, mode, st);
-  return dispatch_self<uint16_t, MmaBf16>(a, d, mode, st);
+  if (io_dtype == P2P_DTYPE_F32) return dispatch_self<float, QkSplit, MmaBf16>(a, d, mode, st);
+  return dispatch_self<uint16_t, QkBf16<uint16_t>, MmaBf16>(a, d, mode, st);
 }
 
-int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, int n_groups, hipStream_t st) {
+int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st) {
   if (compute == P2P_COMPUTE_F32) {
     if (io_dtype != P2P_DTYPE_F32) return P2P_E_DTYPE;
-    return dispatch_cross<float, MmaF32>(a, d, n_groups, st);
+    return dispatch_cross<float, QkF32, MmaF32>(a, d, st);
   }
-  if (io_dtype == P2P_DTYPE_F32) return dispatch_cross<float, MmaBf16>(a, d, n_groups, st);
-  return dispatch_cross<uint16_t, MmaBf16>(a, d, n_groups, st);
+  if (io_dtype == P2P_DTYPE_F32) return dispatch_cross<float, QkSplit, MmaBf16>(a, d, st);
+  return dispatch_cross<uint16_t, QkBf16<uint16_t>, MmaBf16>(a, d, st);
 }
 
 }  // namespace p2p

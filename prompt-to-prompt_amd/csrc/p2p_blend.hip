@@ -92,21 +92,33 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
     pooled[b][pix] = m;
   }
   __syncthreads();
-  // per-image max of the nearest-upsampled maps = max over the sampled source pixels
+  // per-image max of the nearest-upsampled maps: a block-wide max over the upsampled grid
   const float sy = (float)R / (float)a.lat_h, sx = (float)R / (float)a.lat_w;
-  if (tid < 2 * B) {
-    const int b = tid >> 1, which = tid & 1;
-    float m = -INFINITY;
-    for (int Y = 0; Y < a.lat_h; ++Y) {
-      const int y = min((int)floorf(Y * sy), R - 1);
-      for (int X = 0; X < a.lat_w; ++X) {
-        const int x = min((int)floorf(X * sx), R - 1);
-        m = fmaxf(m, which == 0 ? pooled[b][y * R + x] : mean_s[b][y * R + x]);
-      }
+  __shared__ float red[2][256];
+  for (int b = 0; b < B; ++b) {
+    float m0 = -INFINITY, m1 = -INFINITY;
+    for (int yx = tid; yx < HW; yx += blockDim.x) {
+      const int Y = yx / a.lat_w, X = yx - Y * a.lat_w;
+      const int src = min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
+      m0 = fmaxf(m0, pooled[b][src]);
+      m1 = fmaxf(m1, mean_s[b][src]);
     }
-    vmax[b][which] = m;
+    red[0][tid] = m0;
+    red[1][tid] = m1;
+    __syncthreads();
+    for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
+      if (tid < s2) {
+        red[0][tid] = fmaxf(red[0][tid], red[0][tid + s2]);
+        red[1][tid] = fmaxf(red[1][tid], red[1][tid + s2]);
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      vmax[b][0] = red[0][0];
+      vmax[b][1] = red[1][0];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   // masks + latent blend: x_t[b] = x_t[0] + mask * (x_t[b] - x_t[0])
   for (int i = tid; i < B * HW; i += blockDim.x) {
     const int b = i / HW, yx = i - b * HW;
@@ -131,17 +143,15 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
   }
 }
 
-__global__ void store_scale_kernel(const float* __restrict__ src, float* __restrict__ dst, float divisor,
-                                   int64_t n) {
+// dst = src * (1 / divisor): what `tensor / scalar` computes on the reference's cuda:0 device
+// (the f32 reciprocal, then one multiply per element).
+__global__ void store_scale_kernel(const float* __restrict__ src, float* __restrict__ dst, float inv, int64_t n) {
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4_t v = reinterpret_cast<const f32x4_t*>(src)[i];
-    v[0] = v[0] / divisor; v[1] = v[1] / divisor; v[2] = v[2] / divisor; v[3] = v[3] / divisor;
-    reinterpret_cast<f32x4_t*>(dst)[i] = v;
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<f32x4_t*>(dst)[i] = reinterpret_cast<const f32x4_t*>(src)[i] * inv;
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    dst[i] = src[i] / divisor;
+    dst[i] = src[i] * inv;
 }
 
 int run_localblend(const p2p_blend_args& a, hipStream_t st) {
@@ -162,7 +172,8 @@ int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipS
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(store_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, divisor, n);
+  const float inv = 1.0f / divisor;
+  hipLaunchKernelGGL(store_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, inv, n);
   return (int)hipGetLastError();
 }
 

@@ -91,6 +91,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
   CrossArgs a;
   fill_common(a, t);
   int covered = 0;
+  for (int n = 0; n < t->n_batch; ++n) a.ent_group[n] = -1;
   for (int g = 0; g < n_groups; ++g) {
     const p2p_group& G = groups[g];
     if (G.first < 0 || G.count < 1 || G.first + G.count > t->n_batch) return P2P_E_BATCH;
@@ -99,6 +100,10 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     a.grp_count[g] = G.count;
     a.grp_prog[g] = G.program;
     a.grp_alpha[g] = G.alpha;
+    for (int e = G.first; e < G.first + G.count; ++e) {
+      if (a.ent_group[e] >= 0) return P2P_E_BATCH;  // groups overlap
+      a.ent_group[e] = g;
+    }
     covered += G.count;
   }
   if (covered != t->n_batch) return P2P_E_BATCH;
@@ -109,7 +114,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
   }
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;
-  return run_cross(a, t->io_dtype, t->compute, t->head_dim, n_groups, (hipStream_t)stream);
+  return run_cross(a, t->io_dtype, t->compute, t->head_dim, (hipStream_t)stream);
 }
 
 int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* probs, p2p_stream_t stream) {

@@ -110,27 +110,6 @@ struct MmaF32 {
 };
 
 // ------------------------------------------------------------------ global I/O helpers
-// Load 8 consecutive input elements (fp32 or bf16 in HBM) and convert to the MMA element.
-template <typename IO, typename M>
-__device__ __forceinline__ void load8_global(const IO* src, typename M::elem* dst8);
-
-template <>
-__device__ __forceinline__ void load8_global<float, MmaBf16>(const float* src, uint16_t* dst8) {
-  const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
-  const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
-  dst8[0] = f2bf(a[0]); dst8[1] = f2bf(a[1]); dst8[2] = f2bf(a[2]); dst8[3] = f2bf(a[3]);
-  dst8[4] = f2bf(b[0]); dst8[5] = f2bf(b[1]); dst8[6] = f2bf(b[2]); dst8[7] = f2bf(b[3]);
-}
-template <>
-__device__ __forceinline__ void load8_global<uint16_t, MmaBf16>(const uint16_t* src, uint16_t* dst8) {
-  *reinterpret_cast<short8_t*>(dst8) = *reinterpret_cast<const short8_t*>(src);
-}
-template <>
-__device__ __forceinline__ void load8_global<float, MmaF32>(const float* src, float* dst8) {
-  *reinterpret_cast<f32x4_t*>(dst8) = *reinterpret_cast<const f32x4_t*>(src);
-  *reinterpret_cast<f32x4_t*>(dst8 + 4) = *reinterpret_cast<const f32x4_t*>(src + 4);
-}
-
 // Raw register staging: the global bytes of one 8-element chunk, converted at LDS-write time.
 template <typename IO>
 struct Chunk8;
@@ -145,6 +124,7 @@ struct Chunk8<float> {
     a = f32x4_t{0.f, 0.f, 0.f, 0.f};
     b = a;
   }
+  __device__ __forceinline__ float at(int j) const { return j < 4 ? a[j] : b[j - 4]; }
   __device__ __forceinline__ void store(uint16_t* dst) const {
     short8_t v;
     v[0] = (short)f2bf(a[0]); v[1] = (short)f2bf(a[1]); v[2] = (short)f2bf(a[2]); v[3] = (short)f2bf(a[3]);
@@ -154,6 +134,19 @@ struct Chunk8<float> {
   __device__ __forceinline__ void store(float* dst) const {
     *reinterpret_cast<f32x4_t*>(dst) = a;
     *reinterpret_cast<f32x4_t*>(dst + 4) = b;
+  }
+  // split-bf16: hi = bf16(x), lo = bf16(x - hi), written to two planes
+  __device__ __forceinline__ void store_split(uint16_t* hi, uint16_t* lo) const {
+    short8_t vh, vl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = at(j);
+      const uint16_t h = f2bf(x);
+      vh[j] = (short)h;
+      vl[j] = (short)f2bf(x - bf2f(h));
+    }
+    *reinterpret_cast<short8_t*>(hi) = vh;
+    *reinterpret_cast<short8_t*>(lo) = vl;
   }
 };
 template <>
@@ -165,6 +158,106 @@ struct Chunk8<uint16_t> {
   __device__ __forceinline__ void store(float* dst) const {
 #pragma unroll
     for (int j = 0; j < 8; ++j) dst[j] = bf2f((uint16_t)v[j]);
+  }
+};
+
+// ------------------------------------------------------------------ QK^T precision traits
+// How S^T = K Q^T is formed.  K tiles live in LDS in `planes` planes of [rows][KS] elements
+// (plane stride passed at the call site); Q fragments stay in registers.
+//   QkBf16   : bf16 inputs, one bf16 MFMA per 16-deep k step (exact products of bf16 data)
+//   QkSplit  : f32 inputs on the bf16 pipe, split-bf16 x = hi + lo, S = Kh Qh + Kh Ql + Kl Qh
+//              (3 MFMAs; products to ~2^-16 relative, i.e. f32-grade logits)
+//   QkF32    : exact f32 MFMA (check mode)
+template <typename IO>
+struct QkBf16 {
+  using elem = uint16_t;
+  static constexpr int planes = 1;
+  static constexpr int kElemBytes = 2;
+  struct frag {
+    short8_t h;
+  };
+  __device__ __forceinline__ static frag zero() { return frag{short8_t{0, 0, 0, 0, 0, 0, 0, 0}}; }
+  __device__ __forceinline__ static frag load_k(const elem* p, int) {
+    return frag{*reinterpret_cast<const short8_t*>(p)};
+  }
+  __device__ __forceinline__ static frag load_q(const IO* src) {
+    Chunk8<IO> c;
+    c.load(src);
+    frag f;
+    uint16_t tmp[8] __attribute__((aligned(16)));
+    c.store(tmp);
+    f.h = *reinterpret_cast<const short8_t*>(tmp);
+    return f;
+  }
+  __device__ __forceinline__ static void stage(const Chunk8<IO>& c, elem* dst, int) { c.store(dst); }
+  __device__ __forceinline__ static void mma(f32x16_t& acc, const frag& k, const frag& q) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, k.h),
+                                                  __builtin_bit_cast(bf16x8_t, q.h), acc, 0, 0, 0);
+  }
+};
+
+struct QkSplit {
+  using elem = uint16_t;
+  static constexpr int planes = 2;
+  static constexpr int kElemBytes = 2;
+  struct frag {
+    short8_t h, l;
+  };
+  __device__ __forceinline__ static frag zero() {
+    return frag{short8_t{0, 0, 0, 0, 0, 0, 0, 0}, short8_t{0, 0, 0, 0, 0, 0, 0, 0}};
+  }
+  __device__ __forceinline__ static frag load_k(const elem* p, int plane) {
+    return frag{*reinterpret_cast<const short8_t*>(p), *reinterpret_cast<const short8_t*>(p + plane)};
+  }
+  __device__ __forceinline__ static frag load_q(const float* src) {
+    Chunk8<float> c;
+    c.load(src);
+    frag f;
+    uint16_t h[8] __attribute__((aligned(16))), l[8] __attribute__((aligned(16)));
+    c.store_split(h, l);
+    f.h = *reinterpret_cast<const short8_t*>(h);
+    f.l = *reinterpret_cast<const short8_t*>(l);
+    return f;
+  }
+  __device__ __forceinline__ static void stage(const Chunk8<float>& c, elem* dst, int plane) {
+    c.store_split(dst, dst + plane);
+  }
+  __device__ __forceinline__ static void mma(f32x16_t& acc, const frag& k, const frag& q) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, k.l),
+                                                  __builtin_bit_cast(bf16x8_t, q.h), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, k.h),
+                                                  __builtin_bit_cast(bf16x8_t, q.l), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, k.h),
+                                                  __builtin_bit_cast(bf16x8_t, q.h), acc, 0, 0, 0);
+  }
+};
+
+struct QkF32 {
+  using elem = float;
+  static constexpr int planes = 1;
+  static constexpr int kElemBytes = 4;
+  struct frag {
+    float v[8];
+  };
+  __device__ __forceinline__ static frag zero() {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = 0.f;
+    return f;
+  }
+  __device__ __forceinline__ static frag load_k(const elem* p, int) {
+    frag f;
+    const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p);
+    const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + 4);
+    f.v[0] = a[0]; f.v[1] = a[1]; f.v[2] = a[2]; f.v[3] = a[3];
+    f.v[4] = b[0]; f.v[5] = b[1]; f.v[6] = b[2]; f.v[7] = b[3];
+    return f;
+  }
+  __device__ __forceinline__ static frag load_q(const float* src) { return load_k(src, 0); }
+  __device__ __forceinline__ static void stage(const Chunk8<float>& c, elem* dst, int) { c.store(dst); }
+  __device__ __forceinline__ static void mma(f32x16_t& acc, const frag& k, const frag& q) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(k.v[j], q.v[j], acc, 0, 0, 0);
   }
 };
 

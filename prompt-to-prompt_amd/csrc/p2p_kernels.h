@@ -39,6 +39,7 @@ struct CrossArgs {
   float* store;
   int store_accumulate;
   int store_slot[P2P_MAX_BATCH];
+  int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
   int grp_first[P2P_MAX_GROUPS];
   int grp_count[P2P_MAX_GROUPS];
   const void* grp_prog[P2P_MAX_GROUPS];
@@ -48,7 +49,7 @@ struct CrossArgs {
 enum { MODE_FUSED_ = 0, MODE_STORE_ = 1, MODE_PROBS_ = 2, MODE_PV_ = 3 };
 
 int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st);
-int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, int n_groups, hipStream_t st);
+int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
 

@@ -1,7 +1,8 @@
 """HIP kernels vs plain fp32 references (GPU).
 
 Tolerances (north star): attention probabilities within 1e-5 max-abs in the exact-f32 check
-mode and 2e-3 at bf16; outputs O = P V are checked relative to max|V|.
+mode and 2e-3 at bf16; outputs O = P V are checked relative to max|V| (bf16 PV rounds P and
+V to 8 significant bits: |dO| <= 2^-7 max|V|; f32: 1e-5 max|V|).
 """
 import numpy as np
 import pytest
@@ -27,6 +28,10 @@ def ref_out(probs, v, heads):
     vh = v.float().reshape(N, K, heads, C // heads).permute(0, 2, 1, 3)
     o = torch.einsum("nhij,nhjd->nhid", probs, vh)
     return o.permute(0, 2, 1, 3).reshape(N, probs.shape[2], C)
+
+
+def o_tol(v, compute):
+    return (2.0 ** -7 if compute == "bf16" else 1e-5) * v.float().abs().max().item()
 
 
 def make_qkv(N, P, K, heads, d, dtype, qscale=1.0, seed=0, dev="cuda"):
@@ -55,12 +60,11 @@ def test_self_attention_output(cuda, geom, compute):
     torch.cuda.synchronize()
     want = ref_out(ref_probs(q, k, H, scale), v, H)
     err = (o - want).abs().max().item()
-    tol = 2e-5 if compute == "f32" else 2e-2
-    assert err < tol, err
+    assert err < o_tol(v, compute), err
 
 
 @pytest.mark.parametrize("compute,qscale,tol", [("f32", 1.0, 1e-5), ("f32", 12.0, 1e-5),
-                                               ("bf16", 1.0, 2e-3), ("bf16", 8.0, 2e-3)])
+                                               ("bf16", 1.0, 2e-3), ("bf16", 8.0, 2e-3), ("bf16", 16.0, 2e-3)])
 @pytest.mark.parametrize("geom", [(2, 1024, 1024, 2, 80), (2, 256, 256, 4, 160), (2, 64, 4096, 2, 40)],
                          ids=lambda g: "x".join(map(str, g)))
 def test_self_attention_store_probs(cuda, geom, compute, qscale, tol):
@@ -80,7 +84,7 @@ def test_self_attention_store_probs(cuda, geom, compute, qscale, tol):
     err2 = (store - 2 * p.reshape(N * H, P, K)).abs().max().item()
     assert err2 < 2 * tol, err2
     want = ref_out(p, v, H)
-    assert (o - want).abs().max().item() < (2e-5 if compute == "f32" else 2e-2)
+    assert (o - want).abs().max().item() < o_tol(v, compute)
 
 
 def test_self_attention_injection_and_partial_store(cuda):
@@ -93,8 +97,20 @@ def test_self_attention_injection_and_partial_store(cuda):
     slots = [-1, -1, -1, -1, 0, H, 2 * H, 3 * H]
     _hip.self_attn(q, k, v, o, H, scale, compute="f32", qk_src=src, store=store, store_slot=slots)
     p = ref_probs(q, k, H, scale, qk_src=src)
-    assert (o - ref_out(p, v, H)).abs().max().item() < 2e-5
+    assert (o - ref_out(p, v, H)).abs().max().item() < o_tol(v, "f32")
     assert (store - p[4:].reshape(4 * H, P, K)).abs().max().item() < 1e-5
+
+
+def test_bf16_inputs_exact_products(cuda):
+    """bf16 inputs: one bf16 MFMA per k-step multiplies them exactly; the probabilities match
+    an fp32 softmax of the same bf16 data to 2e-3 even on very peaky rows."""
+    N, P, K, H, d = 2, 1024, 1024, 2, 80
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=16.0, seed=21)
+    o = torch.empty_like(q)
+    store = torch.zeros(N * H, P, K, device=cuda)
+    _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16", store=store, store_slot=[0, H])
+    p = ref_probs(q, k, H, d ** -0.5).reshape(N * H, P, K)
+    assert (store - p).abs().max().item() < 2e-3
 
 
 @pytest.mark.parametrize("io", [torch.bfloat16])
@@ -105,7 +121,7 @@ def test_self_attention_bf16_io(cuda, io):
     _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16")
     want = ref_out(ref_probs(q, k, H, d ** -0.5), v, H)
     assert o.dtype == io
-    assert (o.float() - want).abs().max().item() < 3e-2
+    assert (o.float() - want).abs().max().item() < 2 * o_tol(v, "bf16")   # + bf16 output rounding
 
 
 @pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
@@ -122,13 +138,14 @@ def test_probs_and_pv_materialise(cuda, geom, compute, tol):
     o = torch.empty_like(q)
     _hip.attn_pv(probs, v, o, H, compute=compute)
     want = ref_out(probs.reshape(N, H, P, K), v, H)
-    assert (o - want).abs().max().item() < (1e-5 if compute == "f32" else 2e-2)
+    assert (o - want).abs().max().item() < o_tol(v, compute)
 
 
 @pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
-def test_cross_plain_groups(cuda, compute, tol):
-    N, P, K, H, d = 8, 1024, 77, 8, 80
-    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=6.0, seed=13)
+@pytest.mark.parametrize("P", [1024, 100])
+def test_cross_plain_groups(cuda, compute, tol, P):
+    N, K, H, d = 8, 77, 8, 80
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=12.0, seed=13)
     scale = d ** -0.5
     o = torch.empty_like(q)
     store = torch.zeros(N * H, P, K, device=cuda)
@@ -137,7 +154,7 @@ def test_cross_plain_groups(cuda, compute, tol):
                     store_slot=[n * H for n in range(N)])
     p = ref_probs(q, k, H, scale)
     assert (store - p.reshape(N * H, P, K)).abs().max().item() < tol
-    assert (o - ref_out(p, v, H)).abs().max().item() < (2e-5 if compute == "f32" else 2e-2)
+    assert (o - ref_out(p, v, H)).abs().max().item() < o_tol(v, compute)
 
 
 def test_key_mask_materialise(cuda):
@@ -157,6 +174,9 @@ def test_key_mask_materialise(cuda):
 
 
 def test_store_scale(cuda):
+    """get_average_attention divides by cur_step; on cuda:0 (the reference's device) torch
+    multiplies by the f32 reciprocal, which the kernel reproduces bit for bit."""
     x = torch.randn(3, 1000, 77, device=cuda)
-    y = _hip.store_scale(x, 7.0)
-    assert torch.equal(y, x / 7)
+    for steps in (7, 50, 3):
+        y = _hip.store_scale(x, float(steps))
+        assert torch.equal(y, x / steps)

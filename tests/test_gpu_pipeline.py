@@ -1,0 +1,76 @@
+"""End-to-end parity of a full 50-step edit group (north star: final latents cos >= 0.999,
+LocalBlend masks agreeing on >= 99.9 % of pixels) -- GPU.
+
+Product: ptp_utils.text2image_ldm_stable with the fused null_text AttentionReplace +
+LocalBlend (bf16 MFMA kernels).  Checker: the same U-Net weights and seed run through the
+oracle's eager fp32 attention + reference controller semantics + oracle DDIM, written out
+here as a plain loop (ptp_utils.py:65-76, 129-172).  The oracle runs on the GPU with torch
+fp32 ops purely as the checker.
+"""
+import pytest
+import torch
+
+from oracle import control as oc
+from oracle import forward as ofw
+from p2p_amd import config
+from p2p_amd import pipeline as pl
+from p2p_amd import ptp_utils
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_group(model, prompts, x_T, tok, steps=50, guidance=7.5):
+    lb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok)
+    ctrl = oc.OracleController("null", "replace", prompts, steps, 0.8, 0.4, tok, local_blend=lb, store_self=False)
+    dev = model.device
+    ctrl.mapper, ctrl.alpha, lb.alpha = ctrl.mapper.to(dev), ctrl.alpha.to(dev), lb.alpha.to(dev)
+    ofw.install(model, ctrl)
+    B = len(prompts)
+    ids = model.tokenizer(prompts, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    uids = model.tokenizer([""] * B, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    ctx = torch.cat([model.text_encoder(uids)[0], model.text_encoder(ids)[0]])
+    lat = x_T.expand(B, 4, 64, 64).to(dev)
+    sched = model.scheduler
+    sched.set_timesteps(steps)
+    ac = sched.alphas_cumprod.to(dev)
+    with torch.no_grad():
+        for t in sched.timesteps:
+            eps = model.unet(torch.cat([lat] * 2), t, encoder_hidden_states=ctx)["sample"].float()
+            eu, ec = eps.chunk(2)
+            lat = oc.ddim_prev(ac, ac[0], eu + guidance * (ec - eu), int(t), lat)
+            lat = ctrl.step_callback(lat)
+    return lat, lb
+
+
+def cosine(a, b):
+    a, b = a.flatten(1).double(), b.flatten(1).double()
+    return torch.nn.functional.cosine_similarity(a, b, dim=1)
+
+
+@pytest.mark.parametrize("seed", [0])
+def test_edit_group_final_latents(cuda, tok, seed):
+    prompts = pl.north_star_prompts()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
+    x_T = pl.seed_latent(seed)
+    with config.compute_mode("bf16"):
+        ctrl = pl.make_replace_controller(prompts, 50, device=cuda)
+        got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
+    want, _ = oracle_group(model, prompts, x_T, tok)
+    cos = cosine(got, want)
+    print("final-latent cosine per prompt:", [round(c, 6) for c in cos.tolist()])
+    assert torch.isfinite(got).all()
+    assert cos.min().item() >= 0.999, cos
+
+
+def test_edit_group_check_mode_tight(cuda, tok):
+    """exact-f32 kernels: the whole 50-step group tracks the oracle far tighter."""
+    prompts = pl.north_star_prompts()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
+    x_T = pl.seed_latent(3)
+    with config.compute_mode("f32"):
+        ctrl = pl.make_replace_controller(prompts, 50, device=cuda)
+        got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
+    want, _ = oracle_group(model, prompts, x_T, tok)
+    cos = cosine(got, want)
+    print("check-mode final-latent cosine:", [round(c, 8) for c in cos.tolist()])
+    assert cos.min().item() >= 0.99999, cos
