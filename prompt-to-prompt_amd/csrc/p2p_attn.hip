@@ -15,6 +15,13 @@
 
 namespace p2p {
 
+template <typename E>
+__device__ __forceinline__ E one_elem();
+template <>
+__device__ __forceinline__ float one_elem<float>() { return 1.0f; }
+template <>
+__device__ __forceinline__ uint16_t one_elem<uint16_t>() { return 0x3F80; }  // bf16 1.0
+
 // ====================================================================== self attention
 // MODE_FUSED : one online-softmax pass, O = softmax(S) V                        (no map kept)
 // MODE_STORE : pass 1 row max/sum, pass 2 exact P -> store + PV                 (maps kept)
@@ -310,6 +317,218 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
   }
 }
 
+// ====================================================================== fused self attention
+// The hot kernel (G1/G7: P = K = 4096, d = 40).  Differences from self_attn_kernel's FUSED mode:
+//  * row sums come out of the PV MFMA: V's first padding column (d..DV) is set to 1 in LDS, so
+//    O^T row d accumulates sum_k bf16(p_k) -- the same weights the PV uses -- with no VALU adds
+//    (only when DV > D; otherwise the sum is a per-lane VALU sum as before);
+//  * lazy rescale (defer-max): the running max only moves -- and O is only rescaled -- when a
+//    tile's max exceeds it by more than kRescaleThr (log2 units), so p stays <= 2^kRescaleThr;
+//    the decision precedes the tile's exponentiation (the safe order), wave-uniform;
+//  * no key-mask support (materialise mode only) and masking code only for a partial last tile.
+template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a) {
+  using EK = typename MQ::elem;
+  using EV = typename MP::elem;
+  constexpr int DK = (D + 15) / 16 * 16;
+  constexpr int DV = (D + 31) / 32 * 32;
+  constexpr int NKT = DK / 16;
+  constexpr int NDT = DV / 32;
+  constexpr int NSB = BK / 32;
+  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
+  constexpr int VS = (MP::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
+  constexpr int NT = 64 * WAVES;
+  constexpr int CPR = D / 8;
+  constexpr int NCH = (BK * CPR + NT - 1) / NT;
+  constexpr int KPLANE = BK * KS;
+  constexpr int KBUF = KPLANE * MQ::planes;
+  constexpr int VBUF = BK * VS;
+  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
+  constexpr int VBYTES = 2 * VBUF * (int)sizeof(EV);
+  constexpr bool kOnes = DV > D;                 // row sum through the PV MFMA
+  constexpr int kLdt = D / 32;                   // O^T tile / register / lane-half holding row D
+  constexpr int kLrr = D % 32;
+  constexpr int kLh = (kLrr >> 2) & 1;
+  constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+  constexpr float kRescaleThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
+  EK* const Ks = reinterpret_cast<EK*>(smem);
+  EV* const Vs = reinterpret_cast<EV*>(smem + KBYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qi = lane & 31;
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H;
+  const int n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int p = qt * 32 * WAVES + wave * 32 + qi;
+  const bool prow = p < a.P;
+  const int K = a.K;
+  const float c = a.scale_log2;
+
+  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
+
+  // LDS image: zero pads; V column D = 1 in every row of both buffers (the row-sum column)
+  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
+  __syncthreads();
+  if constexpr (kOnes) {
+    for (int r = tid; r < 2 * BK; r += NT) Vs[r * VS + D] = one_elem<EV>();
+  }
+
+  typename MQ::frag qf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int col = 16 * t + 8 * hh;
+    qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+  }
+
+  Chunk8<IO> kreg[NCH], vreg[NCH];
+  // Per-lane element offsets inside a tile are loop-invariant (the tile base advances by a
+  // wave-uniform stride), so no address VGPR is rewritten inside the loop.  Rows past K load
+  // row K-1 instead of a divergent clear path: those keys are masked to -inf, p = 0, and the
+  // duplicated K/V rows never contribute.  Chunk slots past the tile are wave-uniform when
+  // BK*CPR % 64 == 0.
+  // K/V tiles are fetched with range-checked buffer loads: the descriptor spans this (entry,
+  // head)'s rows [tile start, K), so chunks of rows past K read as zeros with no tail logic,
+  // and the per-lane byte offsets stay loop-invariant (a VMEM address VGPR rewritten inside
+  // the loop makes the compiler drain the prefetch with vmcnt(0)).  Chunk slots past the tile
+  // are wave-uniform when BK*CPR % 64 == 0.
+  uint32_t koff[NCH], voff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int cidx = tid + i * NT;
+    const int row = min(cidx / CPR, BK - 1);
+    const int ch = cidx - (cidx / CPR) * CPR;
+    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * (int)sizeof(IO));
+    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * (int)sizeof(IO));
+  }
+  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + D) * (int64_t)sizeof(IO);
+  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
+  const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
+  const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
+  auto stage_load = [&](int kt) {
+    const __amdgpu_buffer_rsrc_t rk =
+        make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
+    const __amdgpu_buffer_rsrc_t rv =
+        make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
+        kreg[i].load_buf(rk, koff[i]);
+        vreg[i].load_buf(rv, voff[i]);
+      }
+    }
+  };
+  auto stage_write = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
+        vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
+      }
+    }
+  };
+
+  const int ntiles = (K + BK - 1) / BK;
+  f32x16_t O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+  float m_run = -INFINITY;  // log2-domain running max (scaled), lagging by < kRescaleThr
+  float l_run = 0.f;        // per-lane partial row sum (only when !kOnes)
+
+  stage_load(0);
+  stage_write(0);
+  // retire every prologue load (Q fragments included) before the loop: otherwise the loop
+  // header merge leaves Q "possibly pending" and the first QK^T waits vmcnt(0), draining the
+  // tile prefetch on every iteration
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_load(kt + 1);
+    float sv[NSB][16];
+    const EK* Kb = Ks + buf * KBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      f32x16_t acc = {};
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+        MQ::mma(acc, fa, qf[t]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
+    }
+    if ((kt + 1) * BK > K) {
+#pragma unroll
+      for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * BK + sb * 32 + acc_row(r, hh) >= K) sv[sb][r] = -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;
+    // defer-max: move the reference point only when this tile overshoots it by > thr
+    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - mnew);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+      l_run *= alpha;
+      m_run = mnew;
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = fast_exp2(fmaf(sv[sb][r], c, -m_run));
+        sv[sb][r] = e;
+        if constexpr (!kOnes) ls += e;
+      }
+    if constexpr (!kOnes) l_run += ls;
+    const EV* Vb = Vs + buf * VBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
+    if (kt + 1 < ntiles) stage_write(buf ^ 1);
+    __syncthreads();
+  }
+  float l;
+  if constexpr (kOnes) l = __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
+  else l = l_run + __shfl_xor(l_run, 32);
+  const float inv = 1.f / l;
+  if (prow) {
+    IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = dt * 32 + 8 * g + 4 * hh;
+        if (dd < D)
+          store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
+                 O[dt][4 * g + 3] * inv);
+      }
+  }
+}
+
 // ====================================================================== cross attention
 // One workgroup = one head x one tile of 32*WAVES queries x one batch entry n.  An edit entry
 // (position b > 0 of a prompt group that carries an edit program) first recomputes the
@@ -550,7 +769,7 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);                                                              \
     dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);                                                        \
     switch (mode) {                                                                                          \
-      case MODE_FUSED: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_FUSED>), grid, block, 0, st, b); break; \
+      case MODE_FUSED: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b); break; \
       case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break; \
       case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break; \
       default: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;         \

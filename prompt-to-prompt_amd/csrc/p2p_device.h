@@ -113,12 +113,24 @@ struct MmaF32 {
 // Raw register staging: the global bytes of one 8-element chunk, converted at LDS-write time.
 template <typename IO>
 struct Chunk8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+// Buffer resource over [base, base + bytes): raw (stride 0) loads past `bytes` return zeros.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  const int n = bytes > 0x7fffffff ? 0x7fffffff : (bytes < 0 ? 0 : (int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+
 template <>
 struct Chunk8<float> {
   f32x4_t a, b;
   __device__ __forceinline__ void load(const float* src) {
     a = *reinterpret_cast<const f32x4_t*>(src);
     b = *reinterpret_cast<const f32x4_t*>(src + 4);
+  }
+  __device__ __forceinline__ void load_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    a = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    b = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off + 16, 0, 0));
   }
   __device__ __forceinline__ void clear() {
     a = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -153,6 +165,9 @@ template <>
 struct Chunk8<uint16_t> {
   short8_t v;
   __device__ __forceinline__ void load(const uint16_t* src) { v = *reinterpret_cast<const short8_t*>(src); }
+  __device__ __forceinline__ void load_buf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    v = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  }
   __device__ __forceinline__ void clear() { v = short8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
   __device__ __forceinline__ void store(uint16_t* dst) const { *reinterpret_cast<short8_t*>(dst) = v; }
   __device__ __forceinline__ void store(float* dst) const {
