@@ -133,20 +133,20 @@ def main():
         ctrl = pl.make_replace_controller(prompts, args.ddim_steps, device=dev)
         return pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(seed), num_steps=args.ddim_steps)
 
-    # seeds partitioned across ranks: rank r runs seeds r, r + world, ...
-    seeds = [rank + world * i for i in range(args.warmup + args.steps)]
-    for s in seeds[:args.warmup]:
+    # groups (seeds) partitioned across ranks round-robin: no collective on the data path
+    from p2p_amd import sweep
+    all_seeds = list(range(world * (args.warmup + args.steps)))
+    mine = sweep.partition(all_seeds, rank, world)
+    for s in mine[:args.warmup]:
         group(s)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timer.enabled = True
     t0 = time.perf_counter()
-    finals = [group(s) for s in seeds[args.warmup:]]
-    lat = torch.stack(finals).float()                       # [steps, 4, 4, 64, 64]
-    if world > 1:
-        gathered = [torch.empty_like(lat) for _ in range(world)]
-        dist.all_gather(gathered, lat)                      # RCCL over xGMI, once per run
+    finals = torch.stack([group(s) for s in mine[args.warmup:]]).float()   # [steps, 4, 4, 64, 64]
+    # one RCCL all-gather of the final latents at the end (the only inter-GPU traffic)
+    gathered = sweep.gather_latents(finals, world * args.steps, world)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -156,6 +156,7 @@ def main():
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
+    assert gathered.shape[0] == world * args.steps and torch.isfinite(gathered).all()
 
     avg_ms, flops, n_launch = timer.summary()
     if rank == 0:

@@ -15,6 +15,15 @@
 
 namespace p2p {
 
+// The value held by lane l ^ 32 (the other half of the wave), via v_permlane32_swap: no LDS
+// round trip (ds_bpermute) on the softmax critical path.
+__device__ __forceinline__ float other_half(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  // r[0]: lanes 0-31 keep x, lanes 32-63 get the low half's x; r[1]: the high half's x everywhere
+  return (threadIdx.x & 32) ? __uint_as_float(r[0]) : __uint_as_float(r[1]);
+}
+
 template <typename E>
 __device__ __forceinline__ E one_elem();
 template <>
@@ -483,7 +492,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
     for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;
+    mx = fmaxf(mx, other_half(mx)) * c;
     // defer-max: move the reference point only when this tile overshoots it by > thr
     if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
       const float mnew = fmaxf(m_run, mx);
@@ -760,16 +769,41 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
 }
 
 // ====================================================================== launchers
+template <typename IO, typename MQ, typename MP, int D, int BK, int W>
+static void launch_fused(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+}
+
 template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
+  if (mode == MODE_FUSED) {
+    // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)
+    if constexpr (BK == 64 && (D == 40 || D == 80)) {
+      if (a.P > 64) {
+        // default: 8 waves x 32 query rows per workgroup, 64-key tiles (measured best at
+        // d = 40 and within 2 % of best at d = 80: tools/attn_bench.py, profiles/)
+        switch (a.variant) {
+          case 1: launch_fused<IO, MQ, MP, D, 64, 4>(a, st); return hipGetLastError();
+          case 2: launch_fused<IO, MQ, MP, D, 128, 4>(a, st); return hipGetLastError();
+          case 3: launch_fused<IO, MQ, MP, D, 128, 8>(a, st); return hipGetLastError();
+          default: launch_fused<IO, MQ, MP, D, 64, 8>(a, st); return hipGetLastError();
+        }
+      }
+    }
+    if (a.P <= 64) launch_fused<IO, MQ, MP, D, BK, 2>(a, st);
+    else launch_fused<IO, MQ, MP, D, BK, 4>(a, st);
+    return hipGetLastError();
+  }
   SelfArgs b = a;
 #define P2P_LAUNCH_SELF(W)                                                                                   \
   {                                                                                                          \
     b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);                                                              \
     dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);                                                        \
     switch (mode) {                                                                                          \
-      case MODE_FUSED: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b); break; \
       case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break; \
       case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break; \
       default: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;         \

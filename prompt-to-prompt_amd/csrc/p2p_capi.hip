@@ -1,6 +1,8 @@
 // extern "C" entry points of libp2p_hip.so (declared in include/p2p_hip.h).
 // Validation happens here, before anything is launched: a rejected call returns a negative
 // P2P_E_* code and touches nothing.
+#include <stdlib.h>
+
 #include "p2p_kernels.h"
 
 using namespace p2p;
@@ -41,6 +43,11 @@ void fill_common(A& a, const p2p_attn_tensors* t) {
   a.store_accumulate = 0;
 }
 
+int self_variant() {
+  const char* e = getenv("P2P_SELF_VARIANT");  // read per call: in-process A/B timing
+  return e ? atoi(e) : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -66,6 +73,7 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
   if (rc) return rc;
   SelfArgs a;
   fill_common(a, t);
+  a.variant = self_variant();
   a.probs = nullptr;
   a.key_mask = nullptr;
   bool any_store = false;
@@ -123,6 +131,7 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
   if (!probs) return P2P_E_ARG;
   SelfArgs a;
   fill_common(a, t);
+  a.variant = 0;
   a.probs = nullptr;
   a.key_mask = key_mask;
   a.store = probs;
@@ -140,6 +149,7 @@ int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stre
   if (!probs) return P2P_E_ARG;
   SelfArgs a;
   fill_common(a, t);
+  a.variant = 0;
   a.probs = probs;
   a.key_mask = nullptr;
   for (int n = 0; n < t->n_batch; ++n) {

@@ -22,6 +22,7 @@ struct SelfArgs {
   const float* probs;          // MODE_PV input [N*H, P, K]
   const uint8_t* key_mask;     // optional [N, K]
   int store_accumulate;
+  int variant;                 // fused-kernel tile shape (P2P_SELF_VARIANT, timing experiments)
   int qk_src[P2P_MAX_BATCH];
   int store_slot[P2P_MAX_BATCH];
 };

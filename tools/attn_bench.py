@@ -52,3 +52,29 @@ def main(dtype=torch.bfloat16, compute="bf16"):
 
 if __name__ == "__main__":
     main()
+    # tile-shape variants of the fused self kernel: in-process A/B, 1 s of warm-up at load,
+    # 6 interleaved rounds of 100 launches each, median per variant
+    import statistics
+    N, H = 8, 8
+    for P, d in ((4096, 40), (1024, 80)):
+        C = H * d
+        q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+        k = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+        v = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+        o = torch.empty_like(q)
+        fn = lambda: _hip.self_attn(q, k, v, o, H, d ** -0.5)  # noqa: E731
+        import time as _t
+        t_end = _t.time() + 1.0
+        while _t.time() < t_end:
+            fn()
+        torch.cuda.synchronize()
+        res = {var: [] for var in range(4)}
+        for rnd in range(6):
+            for var in range(4):
+                os.environ["P2P_SELF_VARIANT"] = str(var)
+                res[var].append(time_fn(fn, iters=100, warm=3))
+        for var in range(4):
+            ms = statistics.median(res[var])
+            print(json.dumps({"variant": var, "P": P, "d": d, "median_ms": round(ms, 4), "min_ms": round(min(res[var]), 4),
+                              "tflops_median": round(4.0 * P * P * C * N / ms / 1e9, 1)}), flush=True)
+        os.environ["P2P_SELF_VARIANT"] = "0"
