@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 1
+#define P2P_ABI_VERSION 2
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -69,7 +69,15 @@ typedef struct {
  * tensor, overwritten (store_accumulate = 0, first step) or added (= 1): the running sum
  * of AttentionStore.between_steps (main.py:135-142). */
 int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store,
-                      const int32_t* store_slot, int32_t store_accumulate, p2p_stream_t stream);
+                      const int32_t* store_slot, int32_t store_accumulate, float* workspace,
+                      p2p_stream_t stream);
+
+/* Bytes of the (nullable) device workspace of p2p_self_attn_fwd.  With a workspace, calls that
+ * keep no maps (bf16 I/O and compute) take the fixed-reference schedule: each softmax row is
+ * exponentiated against the Cauchy-Schwarz bound scale * |q| * max_k |k| of its logits (key
+ * norms computed into the workspace by a first kernel), which removes the running row max and
+ * the rescales from the inner loop; the normalisation divides the reference out. */
+int64_t p2p_self_attn_workspace_size(const p2p_attn_tensors* t);
 
 /* A prompt group of a cross-attention launch: entries [first, first + count) of the batch;
  * entry `first` is the source prompt, the others its edits (main.py:187).  program is the

@@ -26,7 +26,7 @@ MAX_BATCH = 64
 MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class HipError(RuntimeError):
@@ -78,7 +78,9 @@ def lib():
         L.p2p_abi_version.restype = ctypes.c_int
         L.p2p_error_string.restype = ctypes.c_char_p
         L.p2p_error_string.argtypes = [ctypes.c_int]
-        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp]
+        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp, vp]
+        L.p2p_self_attn_workspace_size.argtypes = [ctypes.POINTER(AttnTensors)]
+        L.p2p_self_attn_workspace_size.restype = ctypes.c_int64
         L.p2p_cross_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, i32, vp, vp, i32, vp]
         L.p2p_attn_probs.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp]
         L.p2p_attn_pv.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
@@ -93,7 +95,8 @@ def lib():
     return _lib
 
 
-EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
+EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_self_attn_workspace_size",
+                    "p2p_cross_attn_fwd",
                     "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale")
 
 
@@ -167,11 +170,17 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
     if store is not None:
         _require_cuda(store)
         assert store.dtype == torch.float32 and store.is_contiguous()
+    ws = None
+    if store is None:
+        # key-norm workspace of the fixed-reference schedule (tiny; torch's caching allocator)
+        nbytes = lib().p2p_self_attn_workspace_size(ctypes.byref(t))
+        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
     obs = LAUNCH_OBSERVER
     if obs is not None:
         obs.before("self", t)
     rc = lib().p2p_self_attn_fwd(ctypes.byref(t), src, store.data_ptr() if store is not None else None,
-                                 slots, int(bool(accumulate)), _stream(q.device))
+                                 slots, int(bool(accumulate)), ws.data_ptr() if ws is not None else None,
+                                 _stream(q.device))
     if obs is not None:
         obs.after("self", t)
     _check(rc, "p2p_self_attn_fwd")

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "p2p_hip.h")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(p2p_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(p2p_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_library_exists_and_loads():
@@ -63,14 +63,14 @@ def _tensors(**kw):
 def test_self_attn_rejects(kw, code):
     L = _hip.lib()
     t = _tensors(**kw)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None) == code
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None, None) == code
 
 
 def test_self_attn_rejects_bad_source_index():
     L = _hip.lib()
     t = _tensors()
     src = (ctypes.c_int32 * 8)(0, 1, 2, 3, 4, 5, 6, 99)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None) == -5
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None, None) == -5
 
 
 def test_cross_attn_rejects():
