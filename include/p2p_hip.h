@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 2
+#define P2P_ABI_VERSION 3
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -69,15 +69,7 @@ typedef struct {
  * tensor, overwritten (store_accumulate = 0, first step) or added (= 1): the running sum
  * of AttentionStore.between_steps (main.py:135-142). */
 int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store,
-                      const int32_t* store_slot, int32_t store_accumulate, float* workspace,
-                      p2p_stream_t stream);
-
-/* Bytes of the (nullable) device workspace of p2p_self_attn_fwd.  With a workspace, calls that
- * keep no maps (bf16 I/O and compute) take the fixed-reference schedule: each softmax row is
- * exponentiated against the Cauchy-Schwarz bound scale * |q| * max_k |k| of its logits (key
- * norms computed into the workspace by a first kernel), which removes the running row max and
- * the rescales from the inner loop; the normalisation divides the reference out. */
-int64_t p2p_self_attn_workspace_size(const p2p_attn_tensors* t);
+                      const int32_t* store_slot, int32_t store_accumulate, p2p_stream_t stream);
 
 /* A prompt group of a cross-attention launch: entries [first, first + count) of the batch;
  * entry `first` is the source prompt, the others its edits (main.py:187).  program is the
@@ -130,7 +122,34 @@ typedef struct {
   uint8_t* mask_out;               /* optional [n_prompts, lat_h, lat_w] final mask    */
 } p2p_blend_args;
 
+/* x_t may be NULL when mask_out is given: the mask is computed and nothing is blended (the
+ * latent blend then happens inside p2p_latent_step). */
 int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream);
+
+/* One denoising step's latent update, fused (ptp_utils.py:72-75 diffusion_step tail):
+ *   noise = eps_u + guidance * (eps_c - eps_u)                      (cfg = 1; else noise = eps)
+ *   x0    = (x - sqrt_beta_t * noise) / sqrt_alpha_t                 (null_text.py:475-479:
+ *   out   = sqrt_alpha_prev * x0 + sqrt_one_minus_alpha_prev * noise  prev_step; next_step with
+ *                                                                      the inversion coefficients)
+ *   out[b] = out[0] + mask[b] * (out[b] - out[0])   for b >= 1       (LocalBlend, mask nullable)
+ * eps [cfg ? 2B : B, C, H, W] in eps_dtype (uncond block first, as torch.cat([latents] * 2)),
+ * x / out [B, C, H, W] f32 (out may alias x), mask uint8 [B, H, W] (p2p_localblend mask_out).
+ * The four coefficients are the host-side 0-dim values the scheduler computes (beta_t ** 0.5 ...).
+ * Intermediates are rounded as the reference's eager torch ops round them (bf16 products for a
+ * bf16 eps), so the result is bit-identical to the unfused sequence. */
+typedef struct {
+  const void* eps;
+  int32_t eps_dtype;               /* P2P_DTYPE_*                                      */
+  int32_t cfg;
+  float guidance;
+  const float* x;
+  float* out;
+  int32_t n_prompts, channels, height, width;
+  float sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev;
+  const uint8_t* mask;
+} p2p_latent_step_args;
+
+int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream);
 
 /* AttentionStore.get_average_attention (main.py:144-149): dst = src / divisor, computed as
  * src * (1.0f / divisor) -- what torch does for `cuda_tensor / python_scalar` on the

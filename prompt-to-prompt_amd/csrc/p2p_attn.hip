@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
 //    tile's max exceeds it by more than kRescaleThr (log2 units), so p stays <= 2^kRescaleThr;
 //    the decision precedes the tile's exponentiation (the safe order), wave-uniform;
 //  * no key-mask support (materialise mode only) and masking code only for a partial last tile.
-template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, bool BOUND, int XP = 0>
+template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -399,29 +399,6 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
     qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
   }
 
-  // BOUND: the softmax reference point is the Cauchy-Schwarz bound c * |q| * max_k |k| of the
-  // row's logits (key norms from key_norm_kernel), fixed for the whole row: p <= 1 without a
-  // running max, no max / rescale work in the loop (the normalisation divides it out).
-  float m_fix = 0.f;
-  if constexpr (BOUND) {
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      Chunk8<uint16_t> qc;
-      qc.v = __builtin_bit_cast(short8_t, qf[t]);
-      float tmp[8];
-      qc.store(tmp);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss = fmaf(tmp[j], tmp[j], ss);
-    }
-    ss += other_half(ss);
-    const float* kb = a.kbound + (int64_t)(src * a.H + h) * P2P_KNORM_SPLIT;
-    float kmax = kb[0];
-#pragma unroll
-    for (int i = 1; i < P2P_KNORM_SPLIT; ++i) kmax = fmaxf(kmax, kb[i]);
-    m_fix = c * sqrtf(ss) * kmax;
-  }
-
   Chunk8<IO> kreg[NCH], vreg[NCH];
   // Per-lane element offsets inside a tile are loop-invariant (the tile base advances by a
   // wave-uniform stride), so no address VGPR is rewritten inside the loop.  Rows past K load
@@ -477,18 +454,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
   f32x16_t O[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
-  float m_run = -INFINITY;   // log2-domain reference point (running max lagging by < kRescaleThr)
-  // BOUND: after the first tile the reference stays at that tile's max whenever every logit the
-  // row can still produce is provably within 2^kBoundGap of it (Cauchy-Schwarz bound m_fix):
-  // p <= 2^kBoundGap, no overflow, and p_max >= 1 (no underflow).  Wave-uniform decision; a wave
-  // with a wider row keeps tracking the running max.
-  bool track = true;
-  constexpr float kBoundGap = 64.0f;
+  float m_run = -INFINITY;  // log2-domain running max (scaled), lagging by < kRescaleThr
   float l_run = 0.f;        // per-lane partial row sum (only when !kOnes)
 
-  if constexpr (XP == 2) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WAVES / 2) __builtin_amdgcn_s_setprio(1);
-  }
   stage_load(0);
   stage_write(0);
   // retire every prologue load (Q fragments included) before the loop: otherwise the loop
@@ -519,60 +487,36 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
         for (int r = 0; r < 16; ++r)
           if (kt * BK + sb * 32 + acc_row(r, hh) >= K) sv[sb][r] = -INFINITY;
     }
-    if (track) {
-      float mx = -INFINITY;
+    float mx = -INFINITY;
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
+    for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
-      mx = fmaxf(mx, other_half(mx)) * c;
-      // defer-max: move the reference point only when this tile overshoots it by > thr
-      if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
-        const float mnew = fmaxf(m_run, mx);
-        const float alpha = fast_exp2(m_run - mnew);
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
+    mx = fmaxf(mx, other_half(mx)) * c;
+    // defer-max: move the reference point only when this tile overshoots it by > thr
+    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - mnew);
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
-        l_run *= alpha;
-        m_run = mnew;
-      }
-      if constexpr (BOUND) track = !__all(m_fix - m_run <= kBoundGap);
+        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+      l_run *= alpha;
+      m_run = mnew;
     }
     float ls = 0.f;
 #pragma unroll
     for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        // XP: timing experiments only (P2P_SELF_VARIANT 20-23), wrong results
-        const float e = XP == 1 ? fmaf(sv[sb][r], c, -m_run) * 1.0001f
-                      : XP == 4 ? sv[sb][r] : fast_exp2(fmaf(sv[sb][r], c, -m_run));
+        const float e = fast_exp2(fmaf(sv[sb][r], c, -m_run));
         sv[sb][r] = e;
-        if constexpr (!kOnes || XP == 3) ls += e;
+        if constexpr (!kOnes) ls += e;
       }
-    if constexpr (!kOnes || XP == 3) l_run += ls;
+    if constexpr (!kOnes) l_run += ls;
     const EV* Vb = Vs + buf * VBUF;
-    if constexpr (XP == 5 || XP == 6) {
-      // XP 5: PV MFMAs without the V^T LDS reads; XP 6: the V^T reads without the MFMAs
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const MmaBf16::frag bf = MmaBf16::pack_p(sv[sb] + 8 * s2);
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) {
-            if constexpr (XP == 5) {
-              MmaBf16::mma(O[dt], bf, bf);
-            } else {
-              const MmaBf16::frag af = vt_frag<VS>(Vb, sb * 32, s2, dt * 32, lane);
-              O[dt][0] += __builtin_bit_cast(float, (int)af.v[0] | ((int)af.v[5] << 16));
-            }
-          }
-        }
-    } else if constexpr (XP != 3) {
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
-    }
+    for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
     if (kt + 1 < ntiles) stage_write(buf ^ 1);
     __syncthreads();
   }
@@ -825,75 +769,18 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
 }
 
 // ====================================================================== launchers
-// Per-(entry, head) key norms for the BOUND schedule: kbound[(n*H + h)*SPLIT + s] = max over the
-// s-th key slice of |K[n, key, h*D:(h+1)*D]| (bf16 keys).
-template <int D>
-__global__ __launch_bounds__(256) void key_norm_kernel(SelfArgs a, float* kbound) {
-  const int nh = blockIdx.x;
-  const int s = blockIdx.y;
-  const int h = nh % a.H, n = nh / a.H;
-  const uint16_t* kp = static_cast<const uint16_t*>(a.k) + (int64_t)n * a.bsk + h * D;
-  const int per = (a.K + P2P_KNORM_SPLIT - 1) / P2P_KNORM_SPLIT;
-  const int k0 = s * per, k1 = min(a.K, k0 + per);
-  float mx = 0.f;
-  for (int key = k0 + threadIdx.x; key < k1; key += 256) {
-    float ss = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < D / 8; ++ch) {
-      Chunk8<uint16_t> c8;
-      c8.load(kp + (int64_t)key * a.ldk + ch * 8);
-      float t[8];
-      c8.store(t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss = fmaf(t[j], t[j], ss);
-    }
-    mx = fmaxf(mx, ss);
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // a hair above the exact norm so rounding can never put a logit over the bound
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    kbound[(int64_t)nh * P2P_KNORM_SPLIT + s] = sqrtf(m) * 1.0001f;
-  }
-}
-
 template <typename IO, typename MQ, typename MP, int D, int BK, int W>
 static void launch_fused(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  if constexpr (sizeof(IO) == 2 && MP::kElemBytes == 2) {
-    if (a.kbound) {
-      switch (a.variant) {
-        case 20: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 1>), grid, block, 0, st, b); return;
-        case 21: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 2>), grid, block, 0, st, b); return;
-        case 22: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 3>), grid, block, 0, st, b); return;
-        case 23: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 4>), grid, block, 0, st, b); return;
-        case 24: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 5>), grid, block, 0, st, b); return;
-        case 25: hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true, 6>), grid, block, 0, st, b); return;
-        default: break;
-      }
-      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
   if (mode == MODE_FUSED) {
-    if constexpr (sizeof(IO) == 2 && MP::kElemBytes == 2) {
-      if (a.kbound)   // key norms for the fixed-reference (BOUND) schedules
-        hipLaunchKernelGGL((key_norm_kernel<D>), dim3(a.N * a.H, P2P_KNORM_SPLIT), dim3(256), 0, st, a, a.kbound);
-      hipError_t err;
-      if (launch_self_fast(a, D, st, &err)) return err;
-    }
     // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)
     if constexpr (BK == 64 && (D == 40 || D == 80)) {
       if (a.P > 64) {

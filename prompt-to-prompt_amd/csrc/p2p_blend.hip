@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
     }
     const float mf = mask ? 1.f : 0.f;
     if (a.mask_out) a.mask_out[(int64_t)b * HW + yx] = mask ? 1 : 0;
-    if (b == 0) continue;  // x_t[0] + mask * 0 == x_t[0]
+    if (b == 0 || !a.x_t) continue;  // x_t[0] + mask * 0 == x_t[0]; mask-only mode
     for (int ch = 0; ch < a.channels; ++ch) {
       const float x0 = a.x_t[(int64_t)(0 * a.channels + ch) * HW + yx];
       float* xb = a.x_t + (int64_t)(b * a.channels + ch) * HW + yx;
@@ -154,9 +154,81 @@ __global__ void store_scale_kernel(const float* __restrict__ src, float* __restr
     dst[i] = src[i] * inv;
 }
 
+// ---------------------------------------------------------------- fused latent update
+// One denoising step's latent update (ptp_utils.py:72-75): classifier-free guidance
+// (:73), the DDIM step (diffusers DDIMScheduler.step with eta = 0, restated by the reference as
+// NullInversion.prev_step, null_text.py:471-479; the same formula with the inversion's
+// coefficients is next_step, :481-489) and the LocalBlend latent blend with a precomputed mask
+// (null_text.py:68-70 / main.py:50-52).  Every intermediate is rounded where the reference's
+// torch ops round it: to bf16 for the products torch keeps in the U-Net's bf16 output dtype,
+// to f32 elsewhere, with no fma contraction -- so the update is bit-identical to the eager
+// sequence on the same inputs.
+__device__ __forceinline__ float rnd_bf16(float x) { return bf2f(f2bf(x)); }
+
+// explicit round-to-nearest ops: no fma contraction whatever the compile flags
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a, int64_t chw) {
+  const int HW = a.height * a.width;
+  const int B = a.n_prompts;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto rd = [](float x) { return BF16 ? rnd_bf16(x) : x; };
+  auto ld = [&](int64_t idx) {
+    if constexpr (BF16) return bf2f(static_cast<const uint16_t*>(a.eps)[idx]);
+    else return static_cast<const float*>(a.eps)[idx];
+  };
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < chw; i += stride) {
+    const int yx = (int)(i % HW);
+    float prev0 = 0.f;
+    for (int b = 0; b < B; ++b) {
+      float noise;
+      if (a.cfg) {
+        const float eu = ld((int64_t)b * chw + i);
+        const float ec = ld((int64_t)(B + b) * chw + i);
+        const float diff = rd(sub_rn(ec, eu));
+        const float gd = rd(mul_rn(a.guidance, diff));
+        noise = rd(add_rn(eu, gd));
+      } else {
+        noise = ld((int64_t)b * chw + i);
+      }
+      const float x = a.x[(int64_t)b * chw + i];
+      // a 0-dim f32 factor times a bf16 tensor: torch casts the factor to bf16 first
+      const float t1 = rd(mul_rn(rd(a.sqrt_beta_t), noise));
+      const float x0 = __fdiv_rn(sub_rn(x, t1), a.sqrt_alpha_t);
+      const float dir = rd(mul_rn(rd(a.sqrt_one_minus_alpha_prev), noise));
+      float prev = add_rn(mul_rn(a.sqrt_alpha_prev, x0), dir);
+      if (b == 0) {
+        prev0 = prev;
+      } else if (a.mask) {
+        const float m = a.mask[(int64_t)b * HW + yx] ? 1.f : 0.f;
+        prev = add_rn(prev0, mul_rn(m, sub_rn(prev, prev0)));
+      }
+      a.out[(int64_t)b * chw + i] = prev;
+    }
+  }
+}
+
+int run_latent_step(const p2p_latent_step_args& a, hipStream_t st) {
+  if (!a.eps || !a.x || !a.out || a.n_prompts < 1 || a.channels < 1 || a.height < 1 || a.width < 1)
+    return P2P_E_ARG;
+  if (a.eps_dtype != P2P_DTYPE_F32 && a.eps_dtype != P2P_DTYPE_BF16) return P2P_E_DTYPE;
+  const int64_t chw = (int64_t)a.channels * a.height * a.width;
+  int64_t blocks = (chw + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (a.eps_dtype == P2P_DTYPE_BF16)
+    hipLaunchKernelGGL(latent_step_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
+  else
+    hipLaunchKernelGGL(latent_step_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
+  return (int)hipGetLastError();
+}
+
 int run_localblend(const p2p_blend_args& a, hipStream_t st) {
   if (a.n_prompts < 1 || a.n_prompts > kBlendMaxPrompts || a.map_res * a.map_res > 256 || a.n_words > 128 ||
-      a.n_maps < 1 || a.n_maps > 8 || !a.alpha_layers || !a.x_t || !a.word_sums)
+      a.n_maps < 1 || a.n_maps > 8 || !a.alpha_layers || (!a.x_t && !a.mask_out) || !a.word_sums ||
+      a.lat_h < 1 || a.lat_w < 1)
     return P2P_E_ARG;
   for (int l = 0; l < a.n_maps; ++l)
     if (!a.maps[l]) return P2P_E_ARG;

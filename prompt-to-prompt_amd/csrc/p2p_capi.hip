@@ -67,21 +67,13 @@ const char* p2p_error_string(int code) {
   }
 }
 
-int64_t p2p_self_attn_workspace_size(const p2p_attn_tensors* t) {
-  if (!t || t->n_batch < 1 || t->n_heads < 1) return 0;
-  return (int64_t)t->n_batch * t->n_heads * P2P_KNORM_SPLIT * (int64_t)sizeof(float);
-}
-
 int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store, const int32_t* store_slot,
-                      int32_t store_accumulate, float* workspace, p2p_stream_t stream) {
+                      int32_t store_accumulate, p2p_stream_t stream) {
   int rc = check_tensors(t, true, true, true, true);
   if (rc) return rc;
   SelfArgs a;
   fill_common(a, t);
   a.variant = self_variant();
-  // the fixed-reference (key-norm bound) schedule needs the workspace; variant 9 = online max
-  a.kbound = (workspace && a.variant != 9 && t->io_dtype == P2P_DTYPE_BF16 && t->compute == P2P_COMPUTE_BF16)
-                 ? workspace : nullptr;
   a.probs = nullptr;
   a.key_mask = nullptr;
   bool any_store = false;
@@ -140,7 +132,6 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
   SelfArgs a;
   fill_common(a, t);
   a.variant = 0;
-  a.kbound = nullptr;
   a.probs = nullptr;
   a.key_mask = key_mask;
   a.store = probs;
@@ -159,7 +150,6 @@ int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stre
   SelfArgs a;
   fill_common(a, t);
   a.variant = 0;
-  a.kbound = nullptr;
   a.probs = probs;
   a.key_mask = nullptr;
   for (int n = 0; n < t->n_batch; ++n) {
@@ -172,6 +162,11 @@ int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stre
 int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream) {
   if (!a) return P2P_E_ARG;
   return run_localblend(*a, (hipStream_t)stream);
+}
+
+int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream) {
+  if (!a) return P2P_E_ARG;
+  return run_latent_step(*a, (hipStream_t)stream);
 }
 
 int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream) {

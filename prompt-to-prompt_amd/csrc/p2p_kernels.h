@@ -8,8 +8,6 @@
 
 namespace p2p {
 
-constexpr int P2P_KNORM_SPLIT = 8;  // key slices per (entry, head) in key_norm_kernel
-
 struct SelfArgs {
   const void* q;
   const void* k;
@@ -25,7 +23,6 @@ struct SelfArgs {
   const uint8_t* key_mask;     // optional [N, K]
   int store_accumulate;
   int variant;                 // fused-kernel tile shape (P2P_SELF_VARIANT, timing experiments)
-  float* kbound;               // workspace [N*H*P2P_KNORM_SPLIT] f32: key norms (BOUND schedule) or null
   int qk_src[P2P_MAX_BATCH];
   int store_slot[P2P_MAX_BATCH];
 };
@@ -53,10 +50,9 @@ struct CrossArgs {
 enum { MODE_FUSED_ = 0, MODE_STORE_ = 1, MODE_PROBS_ = 2, MODE_PV_ = 3 };
 
 int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st);
-// p2p_self_fast.hip: the pipelined bf16 schedule for the 64x64 layers (false = not applicable)
-bool launch_self_fast(const SelfArgs& a, int d, hipStream_t st, hipError_t* err);
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
+int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);
 int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
 
 }  // namespace p2p

@@ -26,7 +26,7 @@ MAX_BATCH = 64
 MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class HipError(RuntimeError):
@@ -63,6 +63,17 @@ class BlendArgs(ctypes.Structure):
     ]
 
 
+class LatentArgs(ctypes.Structure):
+    _fields_ = [
+        ("eps", ctypes.c_void_p), ("eps_dtype", ctypes.c_int32), ("cfg", ctypes.c_int32),
+        ("guidance", ctypes.c_float), ("x", ctypes.c_void_p), ("out", ctypes.c_void_p),
+        ("n_prompts", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("width", ctypes.c_int32), ("sqrt_beta_t", ctypes.c_float), ("sqrt_alpha_t", ctypes.c_float),
+        ("sqrt_alpha_prev", ctypes.c_float), ("sqrt_one_minus_alpha_prev", ctypes.c_float),
+        ("mask", ctypes.c_void_p),
+    ]
+
+
 def library_path() -> str:
     return _LIB_PATH
 
@@ -78,16 +89,15 @@ def lib():
         L.p2p_abi_version.restype = ctypes.c_int
         L.p2p_error_string.restype = ctypes.c_char_p
         L.p2p_error_string.argtypes = [ctypes.c_int]
-        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp, vp]
-        L.p2p_self_attn_workspace_size.argtypes = [ctypes.POINTER(AttnTensors)]
-        L.p2p_self_attn_workspace_size.restype = ctypes.c_int64
+        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp]
         L.p2p_cross_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, i32, vp, vp, i32, vp]
         L.p2p_attn_probs.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp]
         L.p2p_attn_pv.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
         L.p2p_localblend.argtypes = [ctypes.POINTER(BlendArgs), vp]
         L.p2p_store_scale.argtypes = [vp, vp, f32, i64, vp]
+        L.p2p_latent_step.argtypes = [ctypes.POINTER(LatentArgs), vp]
         for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
-                   "p2p_localblend", "p2p_store_scale"):
+                   "p2p_localblend", "p2p_store_scale", "p2p_latent_step"):
             getattr(L, fn).restype = ctypes.c_int
         if L.p2p_abi_version() != ABI_VERSION:
             raise HipError(f"libp2p_hip.so ABI {L.p2p_abi_version()} != {ABI_VERSION}")
@@ -95,9 +105,8 @@ def lib():
     return _lib
 
 
-EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_self_attn_workspace_size",
-                    "p2p_cross_attn_fwd",
-                    "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale")
+EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
+                    "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step")
 
 
 def _check(rc: int, what: str):
@@ -170,17 +179,11 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
     if store is not None:
         _require_cuda(store)
         assert store.dtype == torch.float32 and store.is_contiguous()
-    ws = None
-    if store is None:
-        # key-norm workspace of the fixed-reference schedule (tiny; torch's caching allocator)
-        nbytes = lib().p2p_self_attn_workspace_size(ctypes.byref(t))
-        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
     obs = LAUNCH_OBSERVER
     if obs is not None:
         obs.before("self", t)
     rc = lib().p2p_self_attn_fwd(ctypes.byref(t), src, store.data_ptr() if store is not None else None,
-                                 slots, int(bool(accumulate)), ws.data_ptr() if ws is not None else None,
-                                 _stream(q.device))
+                                 slots, int(bool(accumulate)), _stream(q.device))
     if obs is not None:
         obs.after("self", t)
     _check(rc, "p2p_self_attn_fwd")
@@ -230,6 +233,7 @@ def attn_pv(probs, v, o, heads, compute="bf16"):
 
 def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_sub, x_t, word_sums,
                mask_out=None):
+    """LocalBlend on device; x_t None with mask_out given = mask only (no blend)."""
     _require_cuda(x_t, alpha_layers, word_sums, substruct_layers, mask_out, *maps)
     a = BlendArgs()
     for i, m in enumerate(maps):
@@ -244,12 +248,17 @@ def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_
     a.alpha_layers = alpha_layers.data_ptr()
     a.substruct_layers = substruct_layers.data_ptr() if substruct_layers is not None else None
     a.th_pool, a.th_sub = float(th_pool), float(th_sub)
-    assert x_t.dtype == torch.float32 and x_t.is_contiguous()
-    a.x_t = x_t.data_ptr()
-    a.channels, a.lat_h, a.lat_w = x_t.shape[1], x_t.shape[2], x_t.shape[3]
+    if x_t is not None:
+        assert x_t.dtype == torch.float32 and x_t.is_contiguous()
+        a.x_t = x_t.data_ptr()
+        a.channels, a.lat_h, a.lat_w = x_t.shape[1], x_t.shape[2], x_t.shape[3]
+    else:
+        assert mask_out is not None and mask_out.dtype == torch.uint8 and mask_out.is_contiguous()
+        a.x_t = None
+        a.channels, a.lat_h, a.lat_w = 0, mask_out.shape[-2], mask_out.shape[-1]
     a.word_sums = word_sums.data_ptr()
     a.mask_out = mask_out.data_ptr() if mask_out is not None else None
-    rc = lib().p2p_localblend(ctypes.byref(a), _stream(x_t.device))
+    rc = lib().p2p_localblend(ctypes.byref(a), _stream((x_t if x_t is not None else mask_out).device))
     _check(rc, "p2p_localblend")
 
 
@@ -259,4 +268,32 @@ def store_scale(src: torch.Tensor, divisor: float, out: Optional[torch.Tensor] =
     out = torch.empty_like(src) if out is None else out
     rc = lib().p2p_store_scale(src.data_ptr(), out.data_ptr(), float(divisor), src.numel(), _stream(src.device))
     _check(rc, "p2p_store_scale")
+    return out
+
+
+def latent_step(eps, x, out, coeffs, guidance=None, mask=None):
+    """Fused CFG + DDIM step + LocalBlend blend (p2p_latent_step).  eps: [2B or B, C, H, W]
+    (f32/bf16, uncond block first when guidance is given); x, out: f32 [B, C, H, W] (out may be
+    x); coeffs: (sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev) floats;
+    mask: uint8 [B, H, W] or None."""
+    _require_cuda(eps, x, out, mask)
+    for t in (eps, x, out):
+        assert t.is_contiguous()
+    assert x.dtype == torch.float32 and out.dtype == torch.float32 and x.shape == out.shape
+    B, C, H, W = x.shape
+    assert eps.shape[1:] == x.shape[1:] and eps.shape[0] == (2 * B if guidance is not None else B)
+    a = LatentArgs()
+    a.eps, a.eps_dtype = eps.data_ptr(), _dtype_code(eps)
+    a.cfg = 1 if guidance is not None else 0
+    a.guidance = float(guidance) if guidance is not None else 0.0
+    a.x, a.out = x.data_ptr(), out.data_ptr()
+    a.n_prompts, a.channels, a.height, a.width = B, C, H, W
+    a.sqrt_beta_t, a.sqrt_alpha_t, a.sqrt_alpha_prev, a.sqrt_one_minus_alpha_prev = [float(c) for c in coeffs]
+    if mask is not None:
+        assert mask.dtype == torch.uint8 and mask.is_contiguous() and mask.shape[-2:] == (H, W)
+        a.mask = mask.data_ptr()
+    else:
+        a.mask = None
+    rc = lib().p2p_latent_step(ctypes.byref(a), _stream(x.device))
+    _check(rc, "p2p_latent_step")
     return out

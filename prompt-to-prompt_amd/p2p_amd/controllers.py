@@ -80,6 +80,30 @@ def fused_local_blend(x_t, attention_store, alpha_flat, sub_flat, th_pool, th_su
     return out.to(x_t.dtype)
 
 
+def fused_blend_mask(attention_store, alpha_flat, sub_flat, th_pool, th_sub, size):
+    """LocalBlend's final mask [B, H, W] (uint8) only; the latent blend itself then runs inside
+    p2p_latent_step together with the CFG combine and the DDIM step."""
+    maps = list(attention_store["down_cross"][2:4]) + list(attention_store["up_cross"][:3])
+    B = alpha_flat.shape[0]
+    if len(maps) != 5:
+        raise ValueError(f"LocalBlend needs 2 down and 3 up 16x16 cross maps, store has {len(maps)}")
+    heads = maps[0].shape[0] // B
+    maps = [m if (m.dtype == torch.float32 and m.is_contiguous()) else m.float().contiguous() for m in maps]
+    dev = maps[0].device
+    mask = torch.empty(B, *size, dtype=torch.uint8, device=dev)
+    ws = torch.empty(B * 2 * len(maps) * heads * maps[0].shape[1], dtype=torch.float32, device=dev)
+    _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, None, ws, mask_out=mask)
+    return mask
+
+
+def _owned(obj, name) -> bool:
+    """True when ``name`` resolves to a method this library defines (not a user override)."""
+    for owner in type(obj).__mro__:
+        if name in owner.__dict__:
+            return bool(owner.__dict__.get("_P2P_LIB", False))
+    return False
+
+
 def _word_alpha_layers(prompts, words, tokenizer, n_words=MAX_NUM_WORDS):
     a = torch.zeros(len(prompts), 1, 1, 1, 1, n_words)
     for i, (prompt, ws) in enumerate(zip(prompts, words)):
@@ -97,12 +121,21 @@ class LocalBlend:
             raise ValueError("main-form LocalBlend broadcasts only for 2 prompts (see null_text.LocalBlend)")
         return fused_local_blend(x_t, attention_store, self._alpha_flat, None, self.threshold, self.threshold)
 
+    def step_mask(self, attention_store, size):
+        """The blend mask __call__ would apply this step (fused latent-step protocol)."""
+        if self.alpha_layers.shape[0] != 2:
+            raise ValueError("main-form LocalBlend broadcasts only for 2 prompts (see null_text.LocalBlend)")
+        return fused_blend_mask(attention_store, self._alpha_flat, None, self.threshold, self.threshold, size)
+
     def __init__(self, prompts: List[str], words, threshold=.3, tokenizer=None, device=None):
         tokenizer = tokenizer or get_tokenizer()
         device = device or default_device()
         self.alpha_layers = _word_alpha_layers(prompts, words, tokenizer).to(device)
         self._alpha_flat = self.alpha_layers.reshape(len(prompts), -1).contiguous()
         self.threshold = threshold
+
+
+LocalBlend._P2P_LIB = True
 
 
 # ============================================================================ controllers
@@ -113,6 +146,17 @@ class AttentionControl(abc.ABC):
 
     def step_callback(self, x_t):
         return x_t
+
+    def fused_step_mask(self):
+        """Fused latent-step protocol (ptp_utils.diffusion_step): (True, mask_fn) when this
+        step's step_callback is this library's own -- mask_fn(size) then has the callback's
+        side effects and returns the LocalBlend mask or None -- else (False, None)."""
+        if not _owned(self, "step_callback"):
+            return False, None
+        return True, self._step_mask_fn()
+
+    def _step_mask_fn(self):
+        return None
 
     def between_steps(self):
         return
@@ -303,6 +347,20 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         if self.local_blend is not None:
             x_t = self.local_blend(x_t, self.attention_store)
         return x_t
+
+    def _step_mask_fn(self):
+        lb = self.local_blend
+        if lb is None:
+            return None
+        if not (_owned(lb, "__call__") and hasattr(lb, "step_mask")):
+            raise NotFusable
+        return lambda size: lb.step_mask(self.attention_store, size)
+
+    def fused_step_mask(self):
+        try:
+            return super().fused_step_mask()
+        except NotFusable:
+            return False, None
 
     def replace_self_attention(self, attn_base, att_replace):
         if att_replace.shape[2] <= self.SELF_REPLACE_MAX_KEYS:

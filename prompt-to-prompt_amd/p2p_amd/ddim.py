@@ -64,5 +64,21 @@ class DDIMScheduler:
         direction = (1 - a_next) ** 0.5 * model_output
         return a_next ** 0.5 * x0 + direction
 
+    def prev_coeffs(self, timestep):
+        """The four 0-dim factors prev_step multiplies by, as host floats (for p2p_latent_step):
+        (beta_t ** 0.5, a_t ** 0.5, a_prev ** 0.5, (1 - a_prev) ** 0.5), computed by the same
+        f32 tensor ops as prev_step."""
+        t = int(timestep)
+        prev_t = t - self.config.num_train_timesteps // self.num_inference_steps
+        a_t, a_prev = self._coeffs(t, prev_t, torch.device("cpu"))
+        return (float((1 - a_t) ** 0.5), float(a_t ** 0.5), float(a_prev ** 0.5), float((1 - a_prev) ** 0.5))
+
+    def next_coeffs(self, timestep):
+        """The same factors for next_step (DDIM inversion)."""
+        t_next = int(timestep)
+        t = min(t_next - self.config.num_train_timesteps // self.num_inference_steps, 999)
+        a_t, a_next = self._coeffs(t, t_next, torch.device("cpu"))
+        return (float((1 - a_t) ** 0.5), float(a_t ** 0.5), float(a_next ** 0.5), float((1 - a_next) ** 0.5))
+
     def step(self, model_output, timestep, sample, **kw):
         return {"prev_sample": self.prev_step(model_output, timestep, sample)}

@@ -51,6 +51,16 @@ class LocalBlend:
             x_t = _c.fused_local_blend(x_t, attention_store, self._alpha_flat, sub, self.th[0], self.th[1])
         return x_t
 
+    def step_mask(self, attention_store, size):
+        """What __call__ does to its counter, returning the mask it would blend with (or None
+        before start_blend) -- the fused latent-step protocol."""
+        self.counter += 1
+        if self.counter > self.start_blend:
+            self._size = tuple(size)
+            sub = self._sub_flat if self.substruct_layers is not None else None
+            return _c.fused_blend_mask(attention_store, self._alpha_flat, sub, self.th[0], self.th[1], size)
+        return None
+
     def __init__(self, prompts: List[str], words, substruct_words=None, start_blend=0.2, th=(.3, .3),
                  tokenizer=None, device=None):
         tokenizer = tokenizer or get_tokenizer()
@@ -67,11 +77,17 @@ class LocalBlend:
         self.th = th
 
 
+LocalBlend._P2P_LIB = True
+
+
 class EmptyControl:
     """null_text.py:105-114 -- identity, no counters."""
 
     def step_callback(self, x_t):
         return x_t
+
+    def fused_step_mask(self):
+        return (True, None) if _c._owned(self, "step_callback") else (False, None)
 
     def between_steps(self):
         return
@@ -83,6 +99,9 @@ class EmptyControl:
         if type(self).__call__ is not EmptyControl.__call__ or mask is not None:
             return materialized_attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask)
         return plain_attention(q, k, v, heads, scale)
+
+
+EmptyControl._P2P_LIB = True
 
 
 class SpatialReplace(EmptyControl):

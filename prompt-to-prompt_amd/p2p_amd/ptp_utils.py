@@ -21,16 +21,39 @@ from .ptp_words import get_time_words_attention_alpha, get_word_inds, update_alp
 
 # ------------------------------------------------------------------ sampling loop
 def diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource=False):
-    """One CFG denoising step (ptp_utils.py:65-76)."""
+    """One CFG denoising step (ptp_utils.py:65-76).  With this library's DDIM scheduler and a
+    controller whose step_callback is its own, the CFG combine, the DDIM step and LocalBlend's
+    latent blend run as one HIP kernel (p2p_latent_step) -- same result, bit for bit."""
     if low_resource:
         eps_u = model.unet(latents, t, encoder_hidden_states=context[0])["sample"]
         eps_c = model.unet(latents, t, encoder_hidden_states=context[1])["sample"]
+        eps = None
     else:
         eps = model.unet(torch.cat([latents] * 2), t, encoder_hidden_states=context)["sample"]
         eps_u, eps_c = eps.chunk(2)
+    fused = _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidance_scale)
+    if fused is not None:
+        return fused
     noise_pred = eps_u + guidance_scale * (eps_c - eps_u)
     latents = model.scheduler.step(noise_pred, t, latents)["prev_sample"]
     return controller.step_callback(latents)
+
+
+def _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidance_scale):
+    from . import _hip
+    from .ddim import DDIMScheduler
+    if not (isinstance(model.scheduler, DDIMScheduler) and latents.is_cuda and latents.dtype == torch.float32
+            and eps_u.dtype in (torch.float32, torch.bfloat16) and hasattr(controller, "fused_step_mask")):
+        return None
+    ok, mask_fn = controller.fused_step_mask()
+    if not ok:
+        return None
+    if eps is None or not eps.is_contiguous():
+        eps = torch.cat([eps_u, eps_c]).contiguous()
+    x = latents.contiguous()
+    mask = mask_fn(tuple(x.shape[2:])) if mask_fn is not None else None
+    out = torch.empty_like(x)
+    return _hip.latent_step(eps, x, out, model.scheduler.prev_coeffs(t), guidance_scale, mask)
 
 
 def latent2image(vae, latents):

@@ -63,14 +63,14 @@ def _tensors(**kw):
 def test_self_attn_rejects(kw, code):
     L = _hip.lib()
     t = _tensors(**kw)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None, None) == code
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None) == code
 
 
 def test_self_attn_rejects_bad_source_index():
     L = _hip.lib()
     t = _tensors()
     src = (ctypes.c_int32 * 8)(0, 1, 2, 3, 4, 5, 6, 99)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None, None) == -5
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None) == -5
 
 
 def test_cross_attn_rejects():

@@ -41,7 +41,7 @@ def check(var, N, P, K, d, H=8, qscale=1.0, qk_src=None):
 
 
 def main():
-    variants = [int(x) for x in sys.argv[1:]] or [4, 5, 6]
+    variants = [int(x) for x in sys.argv[1:]] or [0, 1, 3]
     cases = [(2, 4096, 4096, 40, 1.0), (2, 4096, 4096, 40, 6.0), (2, 1000, 1000, 40, 3.0), (1, 200, 77, 40, 1.0),
              (1, 100, 33, 40, 12.0), (2, 130, 4096, 40, 2.0)]
     ok = True

@@ -1,5 +1,7 @@
-"""Time one SD-v1.4-shaped U-Net call (batch 8, 64x64 latent) in several layouts/dtypes, with every
-attention call on the HIP kernels (DummyController).  Diagnostic for the caller around the hot path."""
+"""Time one SD-v1.4-shaped U-Net call (batch 8, 64x64 latent, bf16) in several configurations, with
+every attention call on the HIP kernels (DummyController): default layout, channels_last,
+MIOpen find mode (cudnn.benchmark), and a hipGraph replay of the whole call.  Also reports the host
+time to enqueue one call (no sync).  Diagnostic for the caller around the hot path."""
 import os
 import sys
 import time
@@ -11,8 +13,9 @@ import torch  # noqa: E402
 from p2p_amd import pipeline as pl, ptp_utils  # noqa: E402
 
 
-def run(dtype, channels_last, iters=10):
-    m = pl.SyntheticStableDiffusion(device="cuda", dtype=dtype)
+def run(channels_last, benchmark, graph, iters=20):
+    torch.backends.cudnn.benchmark = benchmark
+    m = pl.SyntheticStableDiffusion(device="cuda", dtype=torch.bfloat16)
     if channels_last:
         m.unet = m.unet.to(memory_format=torch.channels_last)
     ptp_utils.register_attention_control(m, None)
@@ -20,18 +23,38 @@ def run(dtype, channels_last, iters=10):
     if channels_last:
         x = x.contiguous(memory_format=torch.channels_last)
     ctx = torch.randn(8, 77, 768, device="cuda")
+    t = torch.tensor([500], device="cuda")
     with torch.no_grad():
         for _ in range(3):
-            m.unet(x, torch.tensor(500), encoder_hidden_states=ctx)
+            m.unet(x, t, encoder_hidden_states=ctx)
+        torch.cuda.synchronize()
+        fn = lambda: m.unet(x, t, encoder_hidden_states=ctx)  # noqa: E731
+        if graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    m.unet(x, t, encoder_hidden_states=ctx)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                m.unet(x, t, encoder_hidden_states=ctx)
+            fn = g.replay
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        enq = time.perf_counter() - t0
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(iters):
-            m.unet(x, torch.tensor(500), encoder_hidden_states=ctx)
+            fn()
         torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / iters * 1e3
+    return (time.perf_counter() - t0) / iters * 1e3, enq * 1e3
 
 
 if __name__ == "__main__":
-    for dtype in (torch.bfloat16,):
-        for cl in (False, True):
-            print(f"unet {dtype} channels_last={cl}: {run(dtype, cl):.2f} ms/call", flush=True)
+    for cl, bm, gr in ((False, False, False), (True, False, False), (True, True, False), (False, True, False),
+                       (True, True, True), (False, False, True)):
+        ms, enq = run(cl, bm, gr)
+        print(f"unet bf16 channels_last={cl} benchmark={bm} graph={gr}: {ms:.2f} ms/call (enqueue {enq:.2f} ms)",
+              flush=True)
