@@ -64,6 +64,20 @@ class DominantKernelTimer:
         return avg_ms, flops, len(ms)
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC pass
+    (profiles/rNN/pmc_g1.json, written from tools/gpu_pmc.sh: FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE).  bench.py cannot collect counters itself (rocprofv3 --pmc is a
+    separate run), so it reports the committed measurement of the same kernel and names it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_g1.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(num_ddim_steps: int):
     """The oracle's fp32 CPU restatement of the same workload on the host cores: ONE denoising
     step (U-Net at batch 8 with the eager patched attention + reference controller +
@@ -162,8 +176,11 @@ def main():
     if rank == 0:
         peak = MFMA_PEAK_BF16_TFLOPS if args.compute == "bf16" else MFMA_PEAK_F32_TFLOPS
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms else None
+        traffic, traffic_src = pmc_traffic()
         roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                    "frac": (achieved / peak) if achieved else None, "traffic": None,
+                    "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                    "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                    "algorithmic_bytes": 4.0 * 8 * 4096 * 320 * 2,
                     "kernel": "self_attn_kernel G1/G7 (P=K=4096, d=40, N=8, H=8)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
