@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 3
+#define P2P_ABI_VERSION 4
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -131,7 +131,9 @@ int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream);
  *   x0    = (x - sqrt_beta_t * noise) / sqrt_alpha_t                 (null_text.py:475-479:
  *   out   = sqrt_alpha_prev * x0 + sqrt_one_minus_alpha_prev * noise  prev_step; next_step with
  *                                                                      the inversion coefficients)
- *   out[b] = out[0] + mask[b] * (out[b] - out[0])   for b >= 1       (LocalBlend, mask nullable)
+ *   out[b] = out[g0] + mask[b] * (out[b] - out[g0])  b not a group's  (LocalBlend, mask nullable;
+ *                                                    first prompt g0     g0 = first prompt of b's
+ *                                                                        group of group_size)
  * eps [cfg ? 2B : B, C, H, W] in eps_dtype (uncond block first, as torch.cat([latents] * 2)),
  * x / out [B, C, H, W] f32 (out may alias x), mask uint8 [B, H, W] (p2p_localblend mask_out).
  * The four coefficients are the host-side 0-dim values the scheduler computes (beta_t ** 0.5 ...).
@@ -147,6 +149,8 @@ typedef struct {
   int32_t n_prompts, channels, height, width;
   float sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev;
   const uint8_t* mask;
+  int32_t group_size;              /* prompts per prompt group (0 = one group of n_prompts) */
+  const uint8_t* group_blend;      /* [n_prompts / group_size] 1 = blend this group, NULL = all */
 } p2p_latent_step_args;
 
 int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream);

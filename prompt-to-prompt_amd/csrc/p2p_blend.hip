@@ -180,10 +180,13 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
     if constexpr (BF16) return bf2f(static_cast<const uint16_t*>(a.eps)[idx]);
     else return static_cast<const float*>(a.eps)[idx];
   };
+  const int gs = a.group_size > 0 ? a.group_size : B;   // prompts per prompt group
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < chw; i += stride) {
     const int yx = (int)(i % HW);
     float prev0 = 0.f;
+    bool blend = false;
     for (int b = 0; b < B; ++b) {
+      const int bg = b % gs;                              // position inside its group
       float noise;
       if (a.cfg) {
         const float eu = ld((int64_t)b * chw + i);
@@ -200,9 +203,10 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
       const float x0 = __fdiv_rn(sub_rn(x, t1), a.sqrt_alpha_t);
       const float dir = rd(mul_rn(rd(a.sqrt_one_minus_alpha_prev), noise));
       float prev = add_rn(mul_rn(a.sqrt_alpha_prev, x0), dir);
-      if (b == 0) {
-        prev0 = prev;
-      } else if (a.mask) {
+      if (bg == 0) {
+        prev0 = prev;                                     // the group's source prompt
+        blend = a.mask && (!a.group_blend || a.group_blend[b / gs]);
+      } else if (blend) {
         const float m = a.mask[(int64_t)b * HW + yx] ? 1.f : 0.f;
         prev = add_rn(prev0, mul_rn(m, sub_rn(prev, prev0)));
       }
@@ -212,7 +216,8 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
 }
 
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st) {
-  if (!a.eps || !a.x || !a.out || a.n_prompts < 1 || a.channels < 1 || a.height < 1 || a.width < 1)
+  if (!a.eps || !a.x || !a.out || a.n_prompts < 1 || a.channels < 1 || a.height < 1 || a.width < 1 ||
+      a.group_size < 0 || (a.group_size > 0 && a.n_prompts % a.group_size))
     return P2P_E_ARG;
   if (a.eps_dtype != P2P_DTYPE_F32 && a.eps_dtype != P2P_DTYPE_BF16) return P2P_E_DTYPE;
   const int64_t chw = (int64_t)a.channels * a.height * a.width;

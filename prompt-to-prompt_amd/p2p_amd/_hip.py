@@ -26,7 +26,7 @@ MAX_BATCH = 64
 MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class HipError(RuntimeError):
@@ -70,7 +70,7 @@ class LatentArgs(ctypes.Structure):
         ("n_prompts", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
         ("width", ctypes.c_int32), ("sqrt_beta_t", ctypes.c_float), ("sqrt_alpha_t", ctypes.c_float),
         ("sqrt_alpha_prev", ctypes.c_float), ("sqrt_one_minus_alpha_prev", ctypes.c_float),
-        ("mask", ctypes.c_void_p),
+        ("mask", ctypes.c_void_p), ("group_size", ctypes.c_int32), ("group_blend", ctypes.c_void_p),
     ]
 
 
@@ -271,11 +271,12 @@ def store_scale(src: torch.Tensor, divisor: float, out: Optional[torch.Tensor] =
     return out
 
 
-def latent_step(eps, x, out, coeffs, guidance=None, mask=None):
+def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, group_blend=None):
     """Fused CFG + DDIM step + LocalBlend blend (p2p_latent_step).  eps: [2B or B, C, H, W]
     (f32/bf16, uncond block first when guidance is given); x, out: f32 [B, C, H, W] (out may be
     x); coeffs: (sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev) floats;
-    mask: uint8 [B, H, W] or None."""
+    mask: uint8 [B, H, W] or None; group_size: prompts per prompt group (0 = one group), with
+    group_blend (uint8 [B / group_size] or None = every group) selecting the groups that blend."""
     _require_cuda(eps, x, out, mask)
     for t in (eps, x, out):
         assert t.is_contiguous()
@@ -294,6 +295,13 @@ def latent_step(eps, x, out, coeffs, guidance=None, mask=None):
         a.mask = mask.data_ptr()
     else:
         a.mask = None
+    a.group_size = int(group_size)
+    if group_blend is not None:
+        _require_cuda(group_blend)
+        assert group_blend.dtype == torch.uint8 and group_blend.numel() * max(group_size, B) >= B
+        a.group_blend = group_blend.data_ptr()
+    else:
+        a.group_blend = None
     rc = lib().p2p_latent_step(ctypes.byref(a), _stream(x.device))
     _check(rc, "p2p_latent_step")
     return out

@@ -17,14 +17,11 @@ from . import _hip
 from . import config
 
 
-def _singles(n):
-    return [(i, 1, None, None) for i in range(n)]
-
-
 def plain_attention(q, k, v, heads, scale, out=None):
     out = torch.empty_like(q) if out is None else out
-    if k.shape[1] <= _hip.MAX_KEYS_CROSS and q.shape[0] <= _hip.MAX_GROUPS:
-        _hip.cross_attn(q, k, v, out, heads, scale, _singles(q.shape[0]), compute=config.COMPUTE)
+    if k.shape[1] <= _hip.MAX_KEYS_CROSS:
+        # one prompt group without an edit program: every entry uses its own probabilities
+        _hip.cross_attn(q, k, v, out, heads, scale, [(0, q.shape[0], None, None)], compute=config.COMPUTE)
     else:
         _hip.self_attn(q, k, v, out, heads, scale, compute=config.COMPUTE)
     return out

@@ -324,8 +324,8 @@ class AttentionStore(AttentionControl):
         store, acc = self._store_target(is_cross, place_in_unet, N - n0, heads, P, K, q.device)
         slots = self._slots(N, n0, heads, store)
         out = torch.empty_like(q)
-        if is_cross and K <= _hip.MAX_KEYS_CROSS and N <= _hip.MAX_GROUPS:
-            groups = [(n, 1, None, None) for n in range(N)]
+        if is_cross and K <= _hip.MAX_KEYS_CROSS:
+            groups = [(0, N, None, None)]
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
                             store_slot=slots, accumulate=acc)
         else:
@@ -425,15 +425,14 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
             raise ValueError(f"controller built for {self.batch_size} prompts got a batch of {n_cond}")
         if is_cross:
             alpha = self.cross_replace_alpha[self.cur_step]
-            if (K > _hip.MAX_KEYS_CROSS or alpha.shape[-1] != K or n0 + 1 > _hip.MAX_GROUPS
-                    or alpha.device != q.device):
+            if K > _hip.MAX_KEYS_CROSS or alpha.shape[-1] != K or alpha.device != q.device:
                 raise NotFusable
             prog = self._device_program(q.device)
         store, acc = self._store_target(is_cross, place_in_unet, n_cond, heads, P, K, q.device)
         slots = self._slots(N, n0, heads, store)
         out = torch.empty_like(q)
         if is_cross:
-            groups = [(n, 1, None, None) for n in range(n0)] + [(n0, n_cond, prog, alpha.contiguous())]
+            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous())]
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
                             store_slot=slots, accumulate=acc)
         else:
@@ -526,6 +525,157 @@ class AttentionReweight(AttentionControlEdit):
 
 
 AttentionReweight._P2P_LIB = True
+
+
+# ============================================================================ prompt-group batching
+class GroupBatch(AttentionControl):
+    """Several prompt groups -- one controller each, built exactly as for a single group -- in
+    ONE U-Net batch (BASELINE.json configs[2]: a batch of edit groups).  The reference runs one
+    group per pipeline call (``self.batch_size = len(prompts)``, main.py:205); this build
+    extension runs G of them per call: the U-Net batch is ``[uncond g0..gG-1 | cond g0..gG-1]``
+    and every attention call is still ONE kernel launch, with one prompt-group descriptor per
+    member (its edit program, its ``cross_replace_alpha[cur_step]`` row, its self-injection
+    source, its AttentionStore slots).  Each member keeps its own counters and its own
+    ``attention_store`` (views into one running-sum tensor per layer), so
+    ``member.get_average_attention()``, ``aggregate_attention`` and LocalBlend work per group
+    unchanged.  Members must take the fused path (library controllers, no LOW_RESOURCE)."""
+
+    _NATIVE = ("__call__", "forward", "between_steps", "step_callback")
+
+    def __init__(self, controllers, group_size: Optional[int] = None):
+        super().__init__()
+        self.members = list(controllers)
+        if not self.members:
+            raise ValueError("GroupBatch needs at least one controller")
+        sizes = {getattr(m, "batch_size", None) for m in self.members}
+        if group_size is None:
+            if len(sizes) != 1 or None in sizes:
+                raise ValueError("pass group_size= (members disagree on / do not know their batch size)")
+            group_size = sizes.pop()
+        self.group_size = int(group_size)
+        for m in self.members:
+            if not (isinstance(m, AttentionControl) and m.fused_supported()):
+                raise ValueError(f"{type(m).__name__}: GroupBatch members must take the fused kernel path")
+        storing = {isinstance(m, AttentionStore) for m in self.members}
+        if len(storing) != 1:
+            raise ValueError("mix of storing and non-storing controllers")
+        self._storing = storing.pop()
+        self._store_self = self._storing and all(m.store_self_maps for m in self.members)
+        self._calls = defaultdict(int)
+        self._combined = defaultdict(list)
+
+    # counters: the composite counts like any controller and moves every member in lockstep
+    @property
+    def num_att_layers(self):
+        return self._num_att_layers
+
+    @num_att_layers.setter
+    def num_att_layers(self, n):
+        self._num_att_layers = n
+        for m in getattr(self, "members", ()):
+            m.num_att_layers = n
+
+    def forward(self, attn, is_cross: bool, place_in_unet: str):
+        raise NotImplementedError("GroupBatch runs only on the fused kernels (no materialised protocol)")
+
+    def between_steps(self):
+        self._calls = defaultdict(int)
+
+    def reset(self):
+        super().reset()
+        for m in getattr(self, "members", ()):
+            m.reset()
+        self._calls = defaultdict(int)
+        self._combined = defaultdict(list)
+
+    def step_callback(self, x_t):
+        B = self.group_size
+        return torch.cat([m.step_callback(x_t[g * B:(g + 1) * B]) for g, m in enumerate(self.members)])
+
+    def fused_step_mask(self):
+        fns = []
+        for m in self.members:
+            ok, fn = m.fused_step_mask()
+            if not ok:
+                return False, None
+            fns.append(fn)
+        if all(fn is None for fn in fns):
+            return True, None
+        B = self.group_size
+
+        def mask_fn(size):
+            masks = [fn(size) if fn is not None else None for fn in fns]
+            if all(mk is None for mk in masks):
+                return None
+            dev = next(mk for mk in masks if mk is not None).device
+            out = torch.zeros(len(masks) * B, *size, dtype=torch.uint8, device=dev)
+            blend = torch.zeros(len(masks), dtype=torch.uint8)
+            for g, mk in enumerate(masks):
+                if mk is not None:
+                    out[g * B:(g + 1) * B] = mk
+                    blend[g] = 1
+            return out, B, blend.to(dev)
+
+        return True, mask_fn
+
+    def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
+        if _low_resource():
+            raise ValueError("GroupBatch does not run with LOW_RESOURCE (one U-Net call per CFG half)")
+        N, P, K = q.shape[0], q.shape[1], k.shape[1]
+        B, G = self.group_size, len(self.members)
+        GB = G * B
+        if N != 2 * GB:
+            raise ValueError(f"GroupBatch of {G} x {B} prompts got a U-Net batch of {N}")
+        store, acc, slots = None, False, None
+        if self._storing and P <= MAX_STORED_QUERIES and (is_cross or self._store_self):
+            key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
+            idx = self._calls[key]
+            self._calls[key] = idx + 1
+            if len(self.members[0].attention_store) == 0:
+                store = torch.empty(GB * heads, P, K, dtype=torch.float32, device=q.device)
+                for g, m in enumerate(self.members):
+                    m.step_store[key].append(store[g * B * heads:(g + 1) * B * heads])
+                self._combined[key].append(store)
+            else:
+                store, acc = self._combined[key][idx], True
+            slots = [-1] * GB + [(n - GB) * heads for n in range(GB, N)]
+        out = torch.empty_like(q)
+        if is_cross and K <= _hip.MAX_KEYS_CROSS:
+            groups = [(0, GB, None, None)]
+            for g, m in enumerate(self.members):
+                first = GB + g * B
+                if isinstance(m, AttentionControlEdit):
+                    alpha = m.cross_replace_alpha[m.cur_step]
+                    if alpha.shape[-1] != K or alpha.device != q.device:
+                        raise ValueError("edit tables do not match this attention call")
+                    groups.append((first, B, m._device_program(q.device), alpha.contiguous()))
+                else:
+                    groups.append((first, B, None, None))
+            _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
+                            store_slot=slots, accumulate=acc)
+        else:
+            qk_src = list(range(N))
+            for g, m in enumerate(self.members):
+                if (isinstance(m, AttentionControlEdit) and not is_cross and m._in_self_window()
+                        and K <= m.SELF_REPLACE_MAX_KEYS):
+                    src = GB + g * B
+                    for b in range(1, B):
+                        qk_src[src + b] = src
+            _hip.self_attn(q, k, v, out, heads, scale, compute=config.COMPUTE, qk_src=qk_src, store=store,
+                           store_slot=slots, accumulate=acc)
+        return out
+
+    def attention(self, q, k, v, heads, scale, is_cross, place_in_unet, mask=None):
+        if mask is not None:
+            raise ValueError("GroupBatch does not take an attention mask")
+        out = self._fused_forward(q, k, v, heads, scale, is_cross, place_in_unet)
+        for m in self.members:
+            m._advance_layer()
+        self._advance_layer()
+        return out
+
+
+GroupBatch._P2P_LIB = True
 
 
 def get_equalizer(text: str, word_select: Union[int, Tuple[int, ...]],

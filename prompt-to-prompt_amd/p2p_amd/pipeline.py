@@ -81,3 +81,49 @@ def run_edit_group(model: SyntheticStableDiffusion, prompts: Sequence[str], cont
     latents, _ = ptp_utils.text2image_ldm_stable(model, list(prompts), controller, num_inference_steps=num_steps,
                                                  guidance_scale=guidance_scale, latent=x_T)
     return latents
+
+
+@torch.no_grad()
+def run_edit_groups(model: SyntheticStableDiffusion, prompt_groups: Sequence[Sequence[str]], controller,
+                    x_Ts: Sequence[torch.Tensor], num_steps: int = 50, guidance_scale: float = 7.5):
+    """G prompt groups (each 1 source + edits, its own seed) denoised in ONE U-Net batch
+    (BASELINE.json configs[2]) with a controllers.GroupBatch: ptp_utils.text2image_ldm_stable's
+    loop (ptp_utils.py:129-172) over the concatenated prompts, the groups' x_T expanded per group
+    (init_latent, ptp_utils.py:88-95).  Returns the final latents [G * B, 4, 64, 64]."""
+    from . import ptp_utils
+    prompts = [p for grp in prompt_groups for p in grp]
+    B = len(prompt_groups[0])
+    if any(len(grp) != B for grp in prompt_groups):
+        raise ValueError("every prompt group needs the same number of prompts")
+    ptp_utils.register_attention_control(model, controller)
+    text = ptp_utils._encode(model, prompts, model.text_encoder)
+    uncond = ptp_utils._encode(model, [""] * len(prompts), model.text_encoder)
+    context = torch.cat([uncond, text])
+    latents = torch.cat([x.reshape(1, 4, 64, 64).expand(B, 4, 64, 64) for x in x_Ts]).to(model.device)
+    model.scheduler.set_timesteps(num_steps)
+    for t in model.scheduler.timesteps:
+        latents = ptp_utils.diffusion_step(model, controller, latents, context, t, guidance_scale)
+    return latents
+
+
+# BASELINE.json configs[2]: AttentionRefine + AttentionReweight (equalizer) groups whose 16/32-res
+# cross maps are all stored.  Each group refines the source prompt by inserted words and
+# reweights one word of it.
+REFINE_SOURCE = "a photo of a house on a mountain"
+REFINE_EDITS = ["a photo of a house on a snowy mountain", "a photo of a wooden house on a mountain",
+                "a photo of a house on a mountain at night"]
+
+
+def make_refine_reweight_controller(prompts: Sequence[str], num_steps: int = 50, word="mountain", value=2.0,
+                                    device=None, tokenizer=None):
+    """AttentionReweight(equalizer) chained on AttentionRefine (main.py:233-278), maps of the
+    16/32-res cross layers kept by the store (self maps off)."""
+    from . import controllers as c
+    tok = tokenizer or c.get_tokenizer()
+    refine = c.AttentionRefine(list(prompts), num_steps, cross_replace_steps=0.8, self_replace_steps=0.4,
+                               tokenizer=tok, device=device)
+    eq = c.get_equalizer(prompts[0], (word,), (value,), tokenizer=tok)
+    ctrl = c.AttentionReweight(list(prompts), num_steps, cross_replace_steps=0.8, self_replace_steps=0.4,
+                               equalizer=eq, controller=refine, tokenizer=tok, device=device)
+    ctrl.store_self_maps = False
+    return ctrl

@@ -52,8 +52,12 @@ def _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidanc
         eps = torch.cat([eps_u, eps_c]).contiguous()
     x = latents.contiguous()
     mask = mask_fn(tuple(x.shape[2:])) if mask_fn is not None else None
+    group_size, group_blend = 0, None
+    if isinstance(mask, tuple):            # prompt-group batch: (mask, group size, groups that blend)
+        mask, group_size, group_blend = mask
     out = torch.empty_like(x)
-    return _hip.latent_step(eps, x, out, model.scheduler.prev_coeffs(t), guidance_scale, mask)
+    return _hip.latent_step(eps, x, out, model.scheduler.prev_coeffs(t), guidance_scale, mask,
+                            group_size, group_blend)
 
 
 def latent2image(vae, latents):
