@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 4
+#define P2P_ABI_VERSION 5
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -102,6 +102,23 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
 
 /* Materialise mode, second half: O[n] = probs[n*H + h] V[n] (ptp_utils.py:206-207). */
 int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stream);
+
+/* Attention with its gradient -- what null-text inversion needs (null_text.py:574-606: Adam on
+ * the null embedding through every patched attention of the U-Net).  Forward: O as
+ * p2p_self_attn_fwd with no controller edit, plus lse [n_batch * n_heads, n_query] f32, the row
+ * log-sum-exp in the log2 domain with the scale folded in (softmax row = exp2(scale * log2(e) *
+ * s - lse)).  Any n_key (self- or cross-attention); bf16 compute only. */
+int p2p_attn_fwd_lse(const p2p_attn_tensors* t, float* lse, p2p_stream_t stream);
+
+/* Backward of O = softmax(Q K^T * scale) V for the same tensors (t->o = the forward's O):
+ *   dV = P^T dO,  dS = P o (dO V^T - rowsum(dO o O)),  dQ = scale dS K,  dK = scale dS^T Q.
+ * dout and dq use q's layout (strides of t->q / t->o); dk, dv are packed [n_batch, n_key,
+ * n_heads * head_dim] in io_dtype, or f32 when kv_f32 = 1 (then they must be zero-filled:
+ * the key/value pass may split the queries over workgroups and add with f32 atomics).
+ * delta: workspace [n_batch * n_heads, n_query] f32.  P is recomputed from lse; bf16 MFMA
+ * operands, f32 accumulation. */
+int p2p_attn_bwd(const p2p_attn_tensors* t, const void* dout, const float* lse, float* delta, void* dq,
+                 void* dk, void* dv, int32_t kv_f32, p2p_stream_t stream);
 
 /* LocalBlend (null_text.py:41-70; main.py:35-52 is the B=2 special case) for one prompt
  * group: maps[l] are the running-sum cross maps of the five 16x16 layers

@@ -535,6 +535,8 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
           store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
                  O[dt][4 * g + 3] * inv);
       }
+    // row log-sum-exp for the backward pass (log2 domain, scale folded: p = exp2(c s - lse))
+    if (a.lse && hh == 0) a.lse[(int64_t)(n * a.H + h) * a.P + p] = m_run + __log2f(l);
   }
 }
 

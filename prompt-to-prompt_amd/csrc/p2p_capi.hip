@@ -74,6 +74,7 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
   SelfArgs a;
   fill_common(a, t);
   a.variant = self_variant();
+  a.lse = nullptr;
   a.probs = nullptr;
   a.key_mask = nullptr;
   bool any_store = false;
@@ -132,6 +133,7 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
   SelfArgs a;
   fill_common(a, t);
   a.variant = 0;
+  a.lse = nullptr;
   a.probs = nullptr;
   a.key_mask = key_mask;
   a.store = probs;
@@ -150,6 +152,7 @@ int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stre
   SelfArgs a;
   fill_common(a, t);
   a.variant = 0;
+  a.lse = nullptr;
   a.probs = probs;
   a.key_mask = nullptr;
   for (int n = 0; n < t->n_batch; ++n) {
@@ -162,6 +165,51 @@ int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stre
 int p2p_localblend(const p2p_blend_args* a, p2p_stream_t stream) {
   if (!a) return P2P_E_ARG;
   return run_localblend(*a, (hipStream_t)stream);
+}
+
+int p2p_attn_fwd_lse(const p2p_attn_tensors* t, float* lse, p2p_stream_t stream) {
+  int rc = check_tensors(t, true, true, true, true);
+  if (rc) return rc;
+  if (!lse) return P2P_E_ARG;
+  if (t->compute != P2P_COMPUTE_BF16) return P2P_E_DTYPE;
+  SelfArgs a;
+  fill_common(a, t);
+  a.variant = 0;
+  a.lse = lse;
+  a.probs = nullptr;
+  a.key_mask = nullptr;
+  for (int n = 0; n < t->n_batch; ++n) {
+    a.qk_src[n] = n;
+    a.store_slot[n] = -1;
+  }
+  return run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_FUSED_, (hipStream_t)stream);
+}
+
+int p2p_attn_bwd(const p2p_attn_tensors* t, const void* dout, const float* lse, float* delta, void* dq,
+                 void* dk, void* dv, int32_t kv_f32, p2p_stream_t stream) {
+  int rc = check_tensors(t, true, true, true, true);
+  if (rc) return rc;
+  if (!dout || !lse || !delta || !dq || !dk || !dv) return P2P_E_ARG;
+  if (t->compute != P2P_COMPUTE_BF16) return P2P_E_DTYPE;
+  if (!aligned16(dout) || !aligned16(dq) || !aligned16(dk) || !aligned16(dv)) return P2P_E_ALIGN;
+  BwdArgs a;
+  a.q = t->q; a.k = t->k; a.v = t->v; a.o = t->o; a.dout = dout;
+  a.dq = dq; a.dk = dk; a.dv = dv; a.lse = lse; a.delta = delta;
+  // dout / dq share q's layout, dk / dv are packed [N, K, H*d]
+  a.ldq = t->q_row_stride; a.ldk = t->k_row_stride; a.ldv = t->v_row_stride; a.ldo = t->o_row_stride;
+  a.lddo = t->o_row_stride; a.lddq = t->q_row_stride;
+  a.bsq = t->q_batch_stride; a.bsk = t->k_batch_stride; a.bsv = t->v_batch_stride; a.bso = t->o_batch_stride;
+  a.bsdo = t->o_batch_stride; a.bsdq = t->q_batch_stride;
+  const int64_t C = (int64_t)t->n_heads * t->head_dim;
+  a.lddk = a.lddv = C;
+  a.bsdk = a.bsdv = C * t->n_key;
+  a.N = t->n_batch; a.P = t->n_query; a.K = t->n_key; a.H = t->n_heads;
+  a.scale = t->scale;
+  a.scale_log2 = t->scale * 1.4426950408889634f;
+  a.n_tiles = 0;
+  a.kv_split = 1;
+  a.kv_f32 = kv_f32 ? 1 : 0;
+  return run_attn_bwd(a, t->io_dtype, t->head_dim, (hipStream_t)stream);
 }
 
 int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream) {

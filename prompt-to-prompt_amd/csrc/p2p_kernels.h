@@ -23,6 +23,7 @@ struct SelfArgs {
   const uint8_t* key_mask;     // optional [N, K]
   int store_accumulate;
   int variant;                 // fused-kernel tile shape (P2P_SELF_VARIANT, timing experiments)
+  float* lse;                  // optional [N*H, P] row log-sum-exp output (fused mode, autograd)
   int qk_src[P2P_MAX_BATCH];
   int store_slot[P2P_MAX_BATCH];
 };
@@ -53,6 +54,22 @@ int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipS
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);
+
+// attention backward (p2p_bwd.hip)
+struct BwdArgs {
+  const void *q, *k, *v, *o, *dout;
+  void *dq, *dk, *dv;          // dq in IO dtype; dk/dv f32 accumulators when kv_split > 1 else IO dtype
+  const float* lse;            // [N*H, P] from the forward
+  float* delta;                // workspace [N*H, P]
+  int64_t ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;   // token strides (elements)
+  int64_t bsq, bsk, bsv, bso, bsdo, bsdq, bsdk, bsdv;   // batch strides (elements)
+  int N, P, K, H;
+  float scale, scale_log2;
+  int n_tiles;                 // launcher-filled
+  int kv_split;                // query splits of the dK/dV pass (>1: f32 atomics into dk/dv)
+  int kv_f32;                  // dk/dv are f32 buffers (atomic or not)
+};
+int run_attn_bwd(const BwdArgs& a, int io_dtype, int d, hipStream_t st);
 int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
 
 }  // namespace p2p

@@ -26,7 +26,7 @@ MAX_BATCH = 64
 MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class HipError(RuntimeError):
@@ -96,8 +96,10 @@ def lib():
         L.p2p_localblend.argtypes = [ctypes.POINTER(BlendArgs), vp]
         L.p2p_store_scale.argtypes = [vp, vp, f32, i64, vp]
         L.p2p_latent_step.argtypes = [ctypes.POINTER(LatentArgs), vp]
+        L.p2p_attn_fwd_lse.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
+        L.p2p_attn_bwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, vp, vp, vp, i32, vp]
         for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
-                   "p2p_localblend", "p2p_store_scale", "p2p_latent_step"):
+                   "p2p_localblend", "p2p_store_scale", "p2p_latent_step", "p2p_attn_fwd_lse", "p2p_attn_bwd"):
             getattr(L, fn).restype = ctypes.c_int
         if L.p2p_abi_version() != ABI_VERSION:
             raise HipError(f"libp2p_hip.so ABI {L.p2p_abi_version()} != {ABI_VERSION}")
@@ -106,7 +108,8 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
-                    "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step")
+                    "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step",
+                    "p2p_attn_fwd_lse", "p2p_attn_bwd")
 
 
 def _check(rc: int, what: str):
@@ -305,3 +308,24 @@ def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, gro
     rc = lib().p2p_latent_step(ctypes.byref(a), _stream(x.device))
     _check(rc, "p2p_latent_step")
     return out
+
+
+def attn_fwd_lse(q, k, v, o, heads, scale, lse):
+    """O and the row log-sum-exp (log2 domain, scale folded) for the backward pass."""
+    t = make_tensors(q, k, v, o, heads, scale, "bf16")
+    _require_cuda(lse)
+    assert lse.dtype == torch.float32 and lse.is_contiguous() and lse.numel() == t.n_batch * heads * t.n_query
+    _check(lib().p2p_attn_fwd_lse(ctypes.byref(t), lse.data_ptr(), _stream(q.device)), "p2p_attn_fwd_lse")
+
+
+def attn_bwd(q, k, v, o, dout, lse, heads, scale, dq, dk, dv, delta):
+    """dq (q's dtype and layout), dk / dv f32 packed [N, K, H*d] (zero-filled: accumulated)."""
+    for x in (q, k, v, o, dout, dq, dk, dv):
+        assert x.is_contiguous()
+    assert dout.shape == o.shape == q.shape and dq.shape == q.shape
+    assert dk.dtype == torch.float32 and dv.dtype == torch.float32 and dk.shape == k.shape and dv.shape == v.shape
+    t = make_tensors(q, k, v, o, heads, scale, "bf16")
+    _require_cuda(dout, lse, delta, dq, dk, dv)
+    rc = lib().p2p_attn_bwd(ctypes.byref(t), dout.data_ptr(), lse.data_ptr(), delta.data_ptr(), dq.data_ptr(),
+                            dk.data_ptr(), dv.data_ptr(), 1, _stream(q.device))
+    _check(rc, "p2p_attn_bwd")

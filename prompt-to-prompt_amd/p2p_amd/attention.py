@@ -17,7 +17,42 @@ from . import _hip
 from . import config
 
 
+class _AttentionFn(torch.autograd.Function):
+    """softmax(Q K^T * scale) V with its gradient on the HIP kernels (p2p_attn_fwd_lse /
+    p2p_attn_bwd) -- what null-text inversion back-propagates through (null_text.py:587-598)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, heads, scale):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        N, P, _ = q.shape
+        o = torch.empty_like(q)
+        lse = torch.empty(N * heads, P, dtype=torch.float32, device=q.device)
+        _hip.attn_fwd_lse(q, k, v, o, heads, scale, lse)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.heads, ctx.scale = heads, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, o, lse = ctx.saved_tensors
+        dout = dout.contiguous().to(q.dtype)
+        dq = torch.empty_like(q)
+        dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+        dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+        delta = torch.empty_like(lse)
+        _hip.attn_bwd(q, k, v, o, dout, lse, ctx.heads, ctx.scale, dq, dk, dv, delta)
+        return dq, dk.to(k.dtype), dv.to(v.dtype), None, None
+
+
+def differentiable_attention(q, k, v, heads, scale):
+    if config.COMPUTE != "bf16":
+        raise NotImplementedError("the attention backward runs on the bf16 kernels only (compute='bf16')")
+    return _AttentionFn.apply(q, k, v, heads, scale)
+
+
 def plain_attention(q, k, v, heads, scale, out=None):
+    if torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad):
+        return differentiable_attention(q, k, v, heads, scale)
     out = torch.empty_like(q) if out is None else out
     if k.shape[1] <= _hip.MAX_KEYS_CROSS:
         # one prompt group without an edit program: every entry uses its own probabilities

@@ -182,3 +182,155 @@ def make_controller(prompts: List[str], is_replace_controller: bool, cross_repla
         eq = get_equalizer(prompts[1], equilizer_params["words"], equilizer_params["values"], tokenizer)
         controller = AttentionReweight(prompts, NUM_DDIM_STEPS, equalizer=eq, controller=controller, **kw)
     return controller
+
+
+# ============================================================================ null-text inversion
+def load_512(image_path, left=0, right=0, top=0, bottom=0):
+    """null_text.py:447-466: crop by the offsets, centre-square, resize to 512 (needs PIL)."""
+    import numpy as np
+    from PIL import Image
+    image = np.array(Image.open(image_path))[:, :, :3] if isinstance(image_path, str) else image_path
+    h, w, _ = image.shape
+    left = min(left, w - 1)
+    right = min(right, w - left - 1)
+    top = min(top, h - left - 1)
+    bottom = min(bottom, h - top - 1)
+    image = image[top:h - bottom, left:w - right]
+    h, w, _ = image.shape
+    if h < w:
+        image = image[:, (w - h) // 2:(w - h) // 2 + h]
+    elif w < h:
+        image = image[(h - w) // 2:(h - w) // 2 + w]
+    return np.array(Image.fromarray(image).resize((512, 512)))
+
+
+class NullInversion:
+    """null_text.py:469-628 on this library's kernels.
+
+    DDIM inversion of the image latent with the conditional U-Net (``ddim_loop``), then, per
+    step, up to ``num_inner_steps`` Adam updates of the null (unconditional) embedding so that
+    the guided DDIM step lands on the inverted trajectory (``null_optimization``).  Every update
+    back-propagates through all 32 patched attentions: the hook is installed with no controller
+    (null_text.py:610), whose plain path is differentiable on the HIP kernels
+    (attention._AttentionFn: p2p_attn_fwd_lse / p2p_attn_bwd).  ``invert`` also takes the image
+    latent itself ([1, 4, H/8, W/8], the form the reference's ``image2latent`` passes through):
+    the synthetic pipeline has no VAE."""
+
+    def __init__(self, model, num_ddim_steps: int = NUM_DDIM_STEPS, guidance_scale: float = GUIDANCE_SCALE):
+        self.model = model
+        self.tokenizer = model.tokenizer
+        self.num_ddim_steps = num_ddim_steps
+        self.guidance_scale = guidance_scale
+        self.model.scheduler.set_timesteps(num_ddim_steps)
+        self.prompt = None
+        self.context = None
+
+    @property
+    def scheduler(self):
+        return self.model.scheduler
+
+    def prev_step(self, model_output, timestep, sample):
+        return self.scheduler.prev_step(model_output, timestep, sample)
+
+    def next_step(self, model_output, timestep, sample):
+        return self.scheduler.next_step(model_output, timestep, sample)
+
+    def get_noise_pred_single(self, latents, t, context):
+        return self.model.unet(latents, t, encoder_hidden_states=context)["sample"]
+
+    def get_noise_pred(self, latents, t, is_forward=True, context=None):
+        context = self.context if context is None else context
+        eps = self.model.unet(torch.cat([latents] * 2), t, encoder_hidden_states=context)["sample"]
+        eps_u, eps_c = eps.chunk(2)
+        g = 1 if is_forward else self.guidance_scale
+        eps = eps_u + g * (eps_c - eps_u)
+        return self.next_step(eps, t, latents) if is_forward else self.prev_step(eps, t, latents)
+
+    @torch.no_grad()
+    def latent2image(self, latents, return_type="np"):
+        vae = getattr(self.model, "vae", None)
+        if vae is None:
+            return None
+        image = vae.decode(1 / 0.18215 * latents.detach())["sample"]
+        if return_type == "np":
+            image = (image / 2 + 0.5).clamp(0, 1).cpu().permute(0, 2, 3, 1).numpy()[0]
+            image = (image * 255).astype("uint8")
+        return image
+
+    @torch.no_grad()
+    def image2latent(self, image):
+        if torch.is_tensor(image) and image.dim() == 4:
+            return image.to(self.model.device)
+        vae = getattr(self.model, "vae", None)
+        if vae is None:
+            raise ValueError("this pipeline has no VAE: pass the image latent [1, 4, H/8, W/8]")
+        import numpy as np
+        x = torch.from_numpy(np.asarray(image)).float() / 127.5 - 1
+        x = x.permute(2, 0, 1).unsqueeze(0).to(self.model.device)
+        return vae.encode(x)["latent_dist"].mean * 0.18215
+
+    @torch.no_grad()
+    def init_prompt(self, prompt: str):
+        def encode(texts):
+            ids = self.tokenizer(texts, padding="max_length", max_length=self.tokenizer.model_max_length,
+                                 truncation=True, return_tensors="pt").input_ids
+            return self.model.text_encoder(ids.to(self.model.device))[0]
+        self.context = torch.cat([encode([""]), encode([prompt])])
+        self.prompt = prompt
+
+    @torch.no_grad()
+    def ddim_loop(self, latent):
+        cond = self.context.chunk(2)[1]
+        trajectory = [latent]
+        latent = latent.clone().detach()
+        ts = self.scheduler.timesteps
+        for i in range(self.num_ddim_steps):
+            t = ts[len(ts) - i - 1]
+            latent = self.next_step(self.get_noise_pred_single(latent, t, cond), t, latent)
+            trajectory.append(latent)
+        return trajectory
+
+    @torch.no_grad()
+    def ddim_inversion(self, image):
+        latent = self.image2latent(image)
+        return self.latent2image(latent), self.ddim_loop(latent)
+
+    def null_optimization(self, latents, num_inner_steps, epsilon):
+        import torch.nn.functional as F
+        uncond, cond = self.context.chunk(2)
+        per_step = []
+        latent_cur = latents[-1]
+        for i in range(self.num_ddim_steps):
+            uncond = uncond.clone().detach().requires_grad_(True)
+            opt = torch.optim.Adam([uncond], lr=1e-2 * (1.0 - i / 100.0))
+            latent_prev = latents[len(latents) - i - 2]
+            t = self.scheduler.timesteps[i]
+            with torch.no_grad():
+                eps_c = self.get_noise_pred_single(latent_cur, t, cond)
+            for _ in range(num_inner_steps):
+                eps_u = self.get_noise_pred_single(latent_cur, t, uncond)
+                eps = eps_u + self.guidance_scale * (eps_c - eps_u)
+                loss = F.mse_loss(self.prev_step(eps, t, latent_cur), latent_prev)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                if loss.item() < epsilon + i * 2e-5:
+                    break
+            per_step.append(uncond[:1].detach())
+            with torch.no_grad():
+                latent_cur = self.get_noise_pred(latent_cur, t, False, torch.cat([uncond, cond]))
+        return per_step
+
+    def invert(self, image, prompt: str, offsets=(0, 0, 0, 0), num_inner_steps=10, early_stop_epsilon=1e-5,
+               verbose=False):
+        from . import ptp_utils
+        self.init_prompt(prompt)
+        ptp_utils.register_attention_control(self.model, None)
+        image_gt = load_512(image, *offsets) if isinstance(image, str) else image
+        if verbose:
+            print("DDIM inversion...")
+        image_rec, ddim_latents = self.ddim_inversion(image_gt)
+        if verbose:
+            print("Null-text optimization...")
+        uncond_embeddings = self.null_optimization(ddim_latents, num_inner_steps, early_stop_epsilon)
+        return (image_gt, image_rec), ddim_latents[-1], uncond_embeddings
