@@ -46,6 +46,36 @@ class SyntheticStableDiffusion:
         self.vae = None
 
 
+class SyntheticLatentDiffusion:
+    """LDM-256 (BASELINE.json configs[0]): the "model" ptp_utils.text2image_ldm expects
+    (``tokenizer``, ``bert``, ``unet``, ``scheduler``, ``vqvae``, ``device``;
+    ptp_utils.py:98-126).  The ldm-text2im-large-256 U-Net is the SD topology with a 1280-d
+    LDMBert context and a 32x32 latent (diffusers config -- external knowledge, not in the
+    container), so every attention layer has P <= 1024 and main.py:131 stores all of them.
+    Random-init weights, seeded embedding-table "LDMBert", DDIM scheduler; no VQ-VAE."""
+
+    def __init__(self, device="cuda", dtype=torch.float32, seed=0):
+        self.device = torch.device(device)
+        self.tokenizer = default_tokenizer()
+        torch.manual_seed(seed)
+        self.unet = UNet2DConditionModel(cross_attention_dim=1280).to(self.device, dtype).eval()
+        for p in self.unet.parameters():
+            p.requires_grad_(False)
+        self.bert = SyntheticTextEncoder(dim=1280, seed=2).to(self.device)
+        self.scheduler = DDIMScheduler(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
+                                       clip_sample=False, set_alpha_to_one=False)
+        self.vqvae = None
+
+
+LDM_PROMPTS = ["A painting of a squirrel eating a burger", "A painting of a squirrel eating a lasagna"]
+
+
+def ldm_seed_latent(seed: int) -> torch.Tensor:
+    """x_T for the 256x256 LDM (init_latent, ptp_utils.py:88-95: [1, 4, 32, 32])."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn((1, 4, 32, 32), generator=g)
+
+
 # The north-star workload (BASELINE.json configs[1]): 1 source + 3 single-word replacements.
 SOURCE = "a painting of a squirrel eating a burger"
 EDITS = ["a painting of a lion eating a burger", "a painting of a cat eating a burger",

@@ -1,0 +1,102 @@
+"""LDM-256 (BASELINE.json configs[0]; ptp_utils.py:98-126) on the fused kernels -- GPU.
+
+32x32 latent, 1280-d context, guidance 7.0, main.py AttentionReplace (self injection for
+K <= 16^2, main.py:170) with every attention map stored (P <= 32^2 everywhere, main.py:131):
+self maps at P = 1024 (d 40), 256 (d 80), 64 and 16 (d 160), cross maps at the same P with 77
+keys.  Checker: the oracle's eager fp32 attention + reference controller + DDIM on the same
+weights (test infrastructure).  Bars: final latents cos >= 0.999 (bf16) / 0.99999 (f32 check
+mode), stored-map averages within 2e-3 max-abs (bf16) after a short run, the same
+dict/list layout, and aggregate_attention over the 16x16 maps.
+"""
+import pytest
+import torch
+
+from oracle import control as oc
+from oracle import forward as ofw
+from p2p_amd import config, controllers
+from p2p_amd import pipeline as pl
+from p2p_amd import ptp_utils
+
+pytestmark = pytest.mark.gpu
+
+GUIDANCE = 7.0
+
+
+def oracle_ldm(model, prompts, x_T, tok, steps):
+    ctrl = oc.OracleController("main", "replace", prompts, steps, 0.8, 0.4, tok)
+    dev = model.device
+    ctrl.mapper, ctrl.alpha = ctrl.mapper.to(dev), ctrl.alpha.to(dev)
+    ofw.install(model, ctrl)
+    B = len(prompts)
+    ids = model.tokenizer(prompts, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    uids = model.tokenizer([""] * B, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    ctx = torch.cat([model.bert(uids)[0], model.bert(ids)[0]])
+    lat = x_T.expand(B, 4, 32, 32).to(dev)
+    sched = model.scheduler
+    sched.set_timesteps(steps)
+    ac = sched.alphas_cumprod.to(dev)
+    with torch.no_grad():
+        for t in sched.timesteps:
+            eps = model.unet(torch.cat([lat] * 2), t, encoder_hidden_states=ctx)["sample"].float()
+            eu, ec = eps.chunk(2)
+            lat = oc.ddim_prev(ac, ac[0], eu + GUIDANCE * (ec - eu), int(t), lat, n_inf=steps)
+    return lat, ctrl
+
+
+def product_ldm(model, prompts, x_T, steps, mode, device):
+    with config.compute_mode(mode):
+        ctrl = controllers.AttentionReplace(prompts, steps, cross_replace_steps=0.8, self_replace_steps=0.4,
+                                            device=device)
+        lat, _ = ptp_utils.text2image_ldm(model, prompts, ctrl, num_inference_steps=steps,
+                                          guidance_scale=GUIDANCE, latent=x_T)
+    return lat, ctrl
+
+
+def cosine(a, b):
+    return torch.nn.functional.cosine_similarity(a.flatten(1).double(), b.flatten(1).double(), dim=1)
+
+
+@pytest.mark.parametrize("mode,bar", [("bf16", 0.999), ("f32", 0.99999)])
+def test_ldm_final_latents(cuda, tok, mode, bar):
+    model = pl.SyntheticLatentDiffusion(device=cuda)
+    x_T = pl.ldm_seed_latent(0)
+    got, ctrl = product_ldm(model, pl.LDM_PROMPTS, x_T, 50, mode, cuda)
+    assert ctrl.num_att_layers == 32 and ctrl.cur_step == 50
+    want, _ = oracle_ldm(model, pl.LDM_PROMPTS, x_T, tok, 50)
+    cos = cosine(got, want)
+    print(f"{mode} final-latent cosine:", [round(c, 7) for c in cos.tolist()])
+    assert torch.isfinite(got).all() and cos.min().item() >= bar, cos
+
+
+def test_ldm_store_all_maps(cuda, tok):
+    """Every layer stored (cross and self, P 1024/256/64/16), post-edit, averaged; aggregate_attention."""
+    model = pl.SyntheticLatentDiffusion(device=cuda)
+    x_T = pl.ldm_seed_latent(1)
+    steps = 3
+    _, ctrl = product_ldm(model, pl.LDM_PROMPTS, x_T, steps, "bf16", cuda)
+    _, octrl = oracle_ldm(model, pl.LDM_PROMPTS, x_T, tok, steps)
+    got, want = ctrl.get_average_attention(), octrl.average()
+    counts = {k: len(v) for k, v in want.items()}
+    assert counts == {"down_cross": 6, "mid_cross": 1, "up_cross": 9,
+                      "down_self": 6, "mid_self": 1, "up_self": 9}, counts
+    worst = 0.0
+    for key in want:
+        assert len(got[key]) == len(want[key]), key
+        for i, (g, w) in enumerate(zip(got[key], want[key])):
+            assert g.shape == w.shape, (key, i, g.shape, w.shape)
+            err = (g.float() - w).abs().max().item()
+            worst = max(worst, err)
+            assert err <= 2e-3, (key, i, tuple(w.shape), err)
+    print("worst stored-map max-abs:", worst)
+    for res in (16, 8):
+        a = controllers.aggregate_attention(ctrl, res, ["up", "down"], True, 1, prompts=pl.LDM_PROMPTS)
+        b = oc_aggregate(want, res, ["up", "down"], 1, len(pl.LDM_PROMPTS))
+        assert a.shape == (res, res, 77) and (a - b).abs().max().item() <= 2e-3
+
+
+def oc_aggregate(avg, res, where, select, n_prompts):
+    """main.py:293-307 on the oracle's averaged store."""
+    maps = [m.reshape(n_prompts, -1, res, res, m.shape[-1])[select]
+            for loc in where for m in avg[f"{loc}_cross"] if m.shape[1] == res ** 2]
+    out = torch.cat(maps, 0)
+    return (out.sum(0) / out.shape[0]).cpu()
