@@ -22,11 +22,14 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 5
+#define P2P_ABI_VERSION 6
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
-#define P2P_PROGRAM_COLS 128 /* column stride of an edit program (>= n_key + 1)      */
+#define P2P_PROGRAM_COLS 128 /* column stride of an edit program (>= n_key)          */
+#define P2P_PROGRAM_TMAX 8   /* term planes per edit (source words per target word)  */
+/* bytes of one edit's record: c_rep f32[COLS] | post f32[COLS] | {i32 row, f32 val}[TMAX][COLS] */
+#define P2P_PROGRAM_REC_BYTES (2 * 4 * P2P_PROGRAM_COLS + 8 * P2P_PROGRAM_TMAX * P2P_PROGRAM_COLS)
 
 enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };
 enum { P2P_COMPUTE_BF16 = 0, P2P_COMPUTE_F32 = 1 };
@@ -73,9 +76,15 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
 
 /* A prompt group of a cross-attention launch: entries [first, first + count) of the batch;
  * entry `first` is the source prompt, the others its edits (main.py:187).  program is the
- * device edit program (layout: P2P_PROGRAM_COLS-strided tables) or NULL
+ * device edit program or NULL
  * for no edit; alpha is the device [count - 1][n_key] row cross_replace_alpha[cur_step]
- * (main.py:189). */
+ * (main.py:189).  Program layout (p2p_amd/programs.py): int32 header {n_edits, n_cols, tmax,
+ * P2P_PROGRAM_COLS}, then per edit e at byte 16 + e * P2P_PROGRAM_REC_BYTES: c_rep f32[COLS],
+ * post f32[COLS], term planes {i32 row, f32 val}[P2P_PROGRAM_TMAX][COLS] -- plane t of column
+ * w is the t-th source row feeding target word w, (0, 0.0) past its last term; tmax <= TMAX is
+ * the number of planes the kernel walks:
+ *   R[w] = post[w] * (c_rep[w] * P_e[w] + sum_{t < tmax} val[t][w] * P_0[row[t][w]])
+ *   P_e'[w] = alpha[w] * R[w] + (1 - alpha[w]) * P_e[w]                                    */
 typedef struct {
   int32_t first;
   int32_t count;

@@ -545,12 +545,15 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 // (position b > 0 of a prompt group that carries an edit program) first recomputes the
 // source prompt's probabilities P0 for the same rows (the K = 77 cross product is cheap) and
 // parks them in LDS, one 32-row slab per wave, so the edit can gather from them:
-//   R[w]  = post[w] * ( c_rep[w] * P_b[w] + sum_t val[t] * P0[rowidx[t]] ),  t in column w
+//   R[w]  = post[w] * ( c_rep[w] * P_b[w] + sum_{t < tmax} val[t][w] * P0[row[t][w]] )
 //   P_b'  = alpha[w] * R[w] + (1 - alpha[w]) * P_b[w]
 // which is AttentionReplace (c_rep 0, mapper column w), AttentionRefine (c_rep 1-a, one term
 // mapper[w] with weight a), AttentionReweight (c_rep 0, term (w, eq[w])), and Reweight
-// chained on either (post = eq) -- host side: p2p_amd/programs.py.  Stored maps leave through
-// the same LDS slab as whole contiguous rows (one [32, K] block per wave).
+// chained on either (post = eq) -- host side: p2p_amd/programs.py.  The term planes make the
+// gather a wave-uniform loop whose loads are independent across the lane's 48 columns.
+// Stored maps leave through the same slab as whole contiguous rows (one [32, K] block per
+// wave).  The slab is dynamic LDS, allocated only by launches with an edit or a store, so a
+// plain launch runs at the occupancy of its K/V tiles alone.
 template <typename IO, typename MQ, typename MP, int D, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
@@ -566,15 +569,13 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
   constexpr int NT = 64 * WAVES;
   constexpr int CPR = D / 8;
   constexpr int NCH = (KR * CPR + NT - 1) / NT;
-  constexpr int P0S = KR + 1;  // odd f32 stride: 32 rows reading one column hit 32 banks
   constexpr int KPLANE = KR * KS;
   constexpr int KBYTES = KPLANE * MQ::planes * (int)sizeof(EK);
   constexpr int VBYTES = KR * VS * (int)sizeof(EV);
-  constexpr int PBYTES = WAVES * 32 * P0S * 4;
-  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + PBYTES];
+  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES];
+  extern __shared__ __attribute__((aligned(16))) char cross_dyn[];  // slab: WAVES * 32 * P0S f32
   EK* const Ks = reinterpret_cast<EK*>(smem);
   EV* const Vs = reinterpret_cast<EV*>(smem + KBYTES);
-  float* const slab = reinterpret_cast<float*>(smem + KBYTES + VBYTES) + (threadIdx.x >> 6) * 32 * P0S;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
   const int qt = logical % a.n_qtiles;
   const int rest = logical / a.n_qtiles;
   const int h = rest % a.H;
-  const int n = rest / a.H;
+  const int n = a.N - 1 - rest / a.H;  // the edits sit last in the batch: dispatch them first
   const int gi = a.ent_group[n];
   const int first = a.grp_first[gi];
   const int b = n - first;
@@ -597,9 +598,29 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
   const bool prow = p < a.P;
   const int K = a.K;
   const float c = a.scale_log2;
+  const int P0S = a.slab_stride;
+  float* const slab = reinterpret_cast<float*>(cross_dyn) + wave * 32 * P0S;
 
-  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
-  __syncthreads();
+  // padding the MFMAs read but the staging never writes (disjoint from it: no extra barrier):
+  // K columns D..DK (multiplied by Q's zero columns) and V rows K..KR (weighted by p = 0)
+  if constexpr (DK > D) {
+    for (int i = tid; i < MQ::planes * KR * (DK - D); i += NT) {
+      const int pl = i / (KR * (DK - D));
+      const int j = i - pl * KR * (DK - D);
+      const int row = j / (DK - D);
+      Ks[pl * KPLANE + row * KS + D + (j - row * (DK - D))] = EK(0);
+    }
+  }
+  for (int i = tid; i < (KR - K) * VS; i += NT) Vs[K * VS + i] = EV(0);
+
+  auto load_q = [&](int e, typename MQ::frag (&qf)[NKT]) {
+    const IO* qp = static_cast<const IO*>(a.q) + (int64_t)e * a.bsq + h * D;
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const int col = 16 * t + 8 * hh;
+      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+    }
+  };
 
   auto stage = [&](int e, bool withV) {
     const IO* kp = static_cast<const IO*>(a.k) + (int64_t)e * a.bsk + h * D;
@@ -627,15 +648,9 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
     }
   };
 
-  // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row
-  auto probs = [&](int e, float (&sv)[KB][16]) {
-    const IO* qp = static_cast<const IO*>(a.q) + (int64_t)e * a.bsq + h * D;
-    typename MQ::frag qf[NKT];
-#pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      const int col = 16 * t + 8 * hh;
-      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
-    }
+  // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row (K rows past
+  // K hold stale LDS: their accumulator rows are replaced by -inf, never used)
+  auto probs = [&](const typename MQ::frag (&qf)[NKT], float (&sv)[KB][16]) {
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
       f32x16_t acc = {};
@@ -669,12 +684,15 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
       for (int r = 0; r < 16; ++r) sv[kb][r] *= inv;
   };
 
+  typename MQ::frag qf[NKT];
   float sv[KB][16];
   if (edit) {
     // ---- source probabilities P0 for these rows -> this wave's LDS slab
+    load_q(first, qf);
     stage(first, false);
     __syncthreads();
-    probs(first, sv);
+    probs(qf, sv);
+    load_q(n, qf);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
@@ -683,38 +701,45 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
         if (w < K) slab[qi * P0S + w] = sv[kb][r];
       }
     __syncthreads();  // slab written; every wave is done reading the source K tile
+  } else {
+    load_q(n, qf);
   }
   stage(n, true);
   __syncthreads();
-  probs(n, sv);
+  probs(qf, sv);
 
   if (edit) {
-    const int* hdr = reinterpret_cast<const int*>(prog);
-    const int n_edits = hdr[0];
-    const int nnz = hdr[2];
-    const float* crep = reinterpret_cast<const float*>(prog + 16);
-    const float* post = crep + n_edits * P2P_PROGRAM_COLS;
-    const int* colptr = reinterpret_cast<const int*>(post + n_edits * P2P_PROGRAM_COLS);
-    const int* rowidx = colptr + n_edits * P2P_PROGRAM_COLS;
-    const float* val = reinterpret_cast<const float*>(rowidx + nnz);
-    const int e = b - 1;
-    const float* ce = crep + e * P2P_PROGRAM_COLS;
-    const float* pe = post + e * P2P_PROGRAM_COLS;
-    const int* cp = colptr + e * P2P_PROGRAM_COLS;
-    const float* al = a.grp_alpha[gi] + e * K;
-    const float* P0 = slab + qi * P0S;
+#pragma clang fp contract(off)
+    const int tmax = reinterpret_cast<const int*>(prog)[2];
+    const char* const rec = prog + 16 + (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES;
+    const float* const ce = reinterpret_cast<const float*>(rec);
+    const float* const pe = ce + P2P_PROGRAM_COLS;
+    const int2* const terms = reinterpret_cast<const int2*>(pe + P2P_PROGRAM_COLS);
+    const float* const al = a.grp_alpha[gi] + (b - 1) * K;
+    const float* const P0 = slab + qi * P0S;
+    float acc[KB][16];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[kb][r] = ce[kb * 32 + acc_row(r, hh)] * sv[kb][r];
+    for (int t = 0; t < tmax; ++t) {  // wave-uniform; padding terms add +0
+      const int2* const plane = terms + t * P2P_PROGRAM_COLS;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int2 tm = plane[kb * 32 + acc_row(r, hh)];
+          acc[kb][r] = acc[kb][r] + __int_as_float(tm.y) * P0[tm.x];
+        }
+    }
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int w = kb * 32 + acc_row(r, hh);
         if (w < K) {
-#pragma clang fp contract(off)
           const float pb = sv[kb][r];
-          float acc = ce[w] * pb;
-          const int t1 = cp[w + 1];
-          for (int t = cp[w]; t < t1; ++t) acc = acc + val[t] * P0[rowidx[t]];
-          const float R = pe[w] * acc;
+          const float R = pe[w] * acc[kb][r];
           const float aw = al[w];
           sv[kb][r] = aw * R + (1.f - aw) * pb;
         }
@@ -738,11 +763,22 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
       float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int count = rows * K;
       if (((uintptr_t)g & 15) == 0 && (count & 3) == 0) {
-        for (int i = lane; i < count / 4; i += 64) {
-          f32x4_t v = reinterpret_cast<const f32x4_t*>(slab)[i];
-          f32x4_t* dst = reinterpret_cast<f32x4_t*>(g) + i;
-          if (a.store_accumulate) v += *dst;
-          *dst = v;
+        // all reads of the running sum first, then all writes: one memory round trip
+        constexpr int IT = (32 * KR / 4 + 63) / 64;
+        const int n4 = count / 4;
+        f32x4_t buf[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+          const int i = lane + 64 * j;
+          if (i < n4) {
+            buf[j] = reinterpret_cast<const f32x4_t*>(slab)[i];
+            if (a.store_accumulate) buf[j] += reinterpret_cast<const f32x4_t*>(g)[i];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+          const int i = lane + 64 * j;
+          if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
         }
       } else {
         for (int i = lane; i < count; i += 64) g[i] = a.store_accumulate ? g[i] + slab[i] : slab[i];
@@ -821,8 +857,12 @@ static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
   constexpr int W = (MP::kElemBytes == 4 && D >= 128) ? 2 : 4;
   CrossArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
+  // the slab holds a [32, K] f32 block per wave: stride K | 1 (odd, so the 32 rows of one
+  // column hit distinct banks) for the edit gather, K for the store rows
+  b.slab_stride = a.K | 1;
+  const size_t slab = a.slab ? (size_t)W * 32 * b.slab_stride * sizeof(float) : 0;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W>), grid, block, slab, st, b);
   return hipGetLastError();
 }
 

@@ -123,6 +123,9 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
   }
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;
+  bool any_edit = false;
+  for (int g = 0; g < n_groups; ++g) any_edit |= groups[g].program != nullptr && groups[g].count > 1;
+  a.slab = (any_store || any_edit) ? 1 : 0;
   return run_cross(a, t->io_dtype, t->compute, t->head_dim, (hipStream_t)stream);
 }
 

@@ -40,6 +40,8 @@ struct CrossArgs {
   int n_qtiles;
   float* store;
   int store_accumulate;
+  int slab;                      // some entry edits or stores: the launch allocates the LDS slab
+  int slab_stride;               // launcher-filled
   int store_slot[P2P_MAX_BATCH];
   int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
   int grp_first[P2P_MAX_GROUPS];

@@ -26,7 +26,8 @@ MAX_BATCH = 64
 MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
-ABI_VERSION = 5
+PROGRAM_TMAX = 8
+ABI_VERSION = 6
 
 
 class HipError(RuntimeError):

@@ -414,7 +414,10 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
     def _device_program(self, device):
         key = str(device)
         if key not in self._program_cache:
-            self._program_cache[key] = self._edit_program().to_device(device)
+            try:
+                self._program_cache[key] = self._edit_program().to_device(device)
+            except ValueError as err:      # beyond the program tables: materialised protocol
+                raise NotFusable from err
         return self._program_cache[key]
 
     def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):

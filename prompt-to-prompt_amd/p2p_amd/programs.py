@@ -17,13 +17,13 @@ Zeros of the dense mapper are skipped, so the column sums are the reference's wi
 zero terms removed (exact for single-entry columns, which is every column the mapper
 builders produce except multi-token source words).
 
-Blob layout (int32/float32 words, P2P_PROGRAM_COLS = 128 column stride):
-    header  int32[4]  = n_edits, n_cols, nnz, 128
-    c_rep   f32 [n_edits][128]
-    post    f32 [n_edits][128]
-    colptr  i32 [n_edits][128]   (column w spans [colptr[w], colptr[w+1]) of the edit's terms)
-    rowidx  i32 [nnz]
-    val     f32 [nnz]
+Blob layout (include/p2p_hip.h; COLS = 128 column stride, TMAX = 8 term planes):
+    header  int32[4] = n_edits, n_cols, tmax, COLS
+    per edit e, at byte 16 + e * REC_BYTES:
+        c_rep f32[COLS] | post f32[COLS] | term {i32 row, f32 val}[TMAX][COLS]
+Plane t of column w holds the t-th term of that column, (0, 0.0) past its last one; the kernel
+walks the first ``tmax`` planes for every column (a wave-uniform loop of independent loads), and
+the padding adds +0.0 after the real terms, so the sums keep the sparse order exactly.
 """
 from __future__ import annotations
 
@@ -34,6 +34,8 @@ import numpy as np
 import torch
 
 PROGRAM_COLS = 128
+PROGRAM_TMAX = 8
+REC_BYTES = 2 * 4 * PROGRAM_COLS + 8 * PROGRAM_TMAX * PROGRAM_COLS
 
 
 @dataclass
@@ -44,28 +46,28 @@ class EditProgram:
     post: np.ndarray                # [E, n_cols] f32
     terms: List[List[List[tuple]]] = field(default_factory=list)  # [E][w] -> [(row, val)]
 
+    @property
+    def tmax(self) -> int:
+        return max([len(col) for cols in self.terms for col in cols] + [0])
+
     def blob(self) -> np.ndarray:
         E, n = self.n_edits, self.n_cols
-        if n + 1 > PROGRAM_COLS:
+        if n > PROGRAM_COLS:
             raise ValueError(f"{n} words exceed the program column stride {PROGRAM_COLS}")
-        c_rep = np.zeros((E, PROGRAM_COLS), np.float32)
-        post = np.zeros((E, PROGRAM_COLS), np.float32)
-        colptr = np.zeros((E, PROGRAM_COLS), np.int32)
-        rows, vals = [], []
+        tmax = self.tmax
+        if tmax > PROGRAM_TMAX:
+            raise ValueError(f"a target word gathers {tmax} source words (> {PROGRAM_TMAX})")
+        rec = np.zeros((E, REC_BYTES // 4), np.uint32)
         for e in range(E):
-            c_rep[e, :n] = self.c_rep[e]
-            post[e, :n] = self.post[e]
+            rec[e, :n] = np.asarray(self.c_rep[e], np.float32).view(np.uint32)
+            rec[e, PROGRAM_COLS:PROGRAM_COLS + n] = np.asarray(self.post[e], np.float32).view(np.uint32)
+            planes = rec[e, 2 * PROGRAM_COLS:].reshape(PROGRAM_TMAX, PROGRAM_COLS, 2)
             for w in range(n):
-                colptr[e, w] = len(rows)
-                for (r, v) in self.terms[e][w]:
-                    rows.append(r)
-                    vals.append(v)
-            colptr[e, n:] = len(rows)
-        header = np.array([E, n, len(rows), PROGRAM_COLS], np.int32)
-        parts = [header.view(np.uint8), c_rep.view(np.uint8).ravel(), post.view(np.uint8).ravel(),
-                 colptr.view(np.uint8).ravel(), np.array(rows, np.int32).view(np.uint8),
-                 np.array(vals, np.float32).view(np.uint8)]
-        return np.concatenate(parts)
+                for t, (r, v) in enumerate(self.terms[e][w]):
+                    planes[t, w, 0] = np.uint32(np.int32(r).view(np.uint32))
+                    planes[t, w, 1] = np.float32(v).view(np.uint32)
+        header = np.array([E, n, tmax, PROGRAM_COLS], np.int32)
+        return np.concatenate([header.view(np.uint8), rec.view(np.uint8).ravel()])
 
     def to_device(self, device) -> torch.Tensor:
         return torch.from_numpy(self.blob().copy()).to(device)

@@ -14,23 +14,23 @@ COLS = programs.PROGRAM_COLS
 
 
 def run_blob(blob: np.ndarray, P0: np.ndarray, Pb: np.ndarray, alpha: np.ndarray) -> np.ndarray:
-    """Reference interpreter of the kernel's edit step (p2p_attn.hip cross_attn_kernel)."""
+    """Reference interpreter of the kernel's edit step (p2p_attn.hip cross_attn_kernel): every
+    column walks the first tmax term planes."""
     hdr = blob[:16].view(np.int32)
-    E, n, nnz = int(hdr[0]), int(hdr[1]), int(hdr[2])
-    off = 16
-    crep = blob[off:off + 4 * E * COLS].view(np.float32).reshape(E, COLS); off += 4 * E * COLS
-    post = blob[off:off + 4 * E * COLS].view(np.float32).reshape(E, COLS); off += 4 * E * COLS
-    colptr = blob[off:off + 4 * E * COLS].view(np.int32).reshape(E, COLS); off += 4 * E * COLS
-    rowidx = blob[off:off + 4 * nnz].view(np.int32); off += 4 * nnz
-    val = blob[off:off + 4 * nnz].view(np.float32)
+    E, n, tmax = int(hdr[0]), int(hdr[1]), int(hdr[2])
     out = Pb.copy()                                   # [E, H, P, n]
     for e in range(E):
+        rec = blob[16 + e * programs.REC_BYTES:16 + (e + 1) * programs.REC_BYTES]
+        crep = rec[:4 * COLS].view(np.float32)
+        post = rec[4 * COLS:8 * COLS].view(np.float32)
+        planes = rec[8 * COLS:].view(np.int32).reshape(programs.PROGRAM_TMAX, COLS, 2)
         for w in range(n):
             pb = Pb[e, ..., w]
-            acc = (crep[e, w] * pb).astype(np.float32)
-            for t in range(colptr[e, w], colptr[e, w + 1]):
-                acc = (acc + np.float32(val[t]) * P0[..., rowidx[t]]).astype(np.float32)
-            R = (post[e, w] * acc).astype(np.float32)
+            acc = (crep[w] * pb).astype(np.float32)
+            for t in range(tmax):
+                row, val = int(planes[t, w, 0]), planes[t, w, 1:2].view(np.float32)[0]
+                acc = (acc + np.float32(val) * P0[..., row]).astype(np.float32)
+            R = (post[w] * acc).astype(np.float32)
             a = np.float32(alpha[e, w])
             out[e, ..., w] = (a * R + (np.float32(1) - a) * pb).astype(np.float32)
     return out
@@ -134,7 +134,20 @@ def test_fused_support_detection(tok):
 def test_program_blob_layout():
     m = torch.zeros(2, 77, 77)
     m[:, torch.arange(77), torch.arange(77)] = 1
+    m[1, 5, 6] = 0.5                                  # column 6 of edit 1 gathers two rows
+    m[1, 6, 6] = 0.5
     blob = programs.replace_program(m).blob()
     hdr = blob[:16].view(np.int32)
-    assert hdr.tolist() == [2, 77, 154, COLS]
-    assert blob.nbytes == 16 + 3 * 4 * 2 * COLS + 8 * 154
+    assert hdr.tolist() == [2, 77, 2, COLS]
+    assert blob.nbytes == 16 + 2 * programs.REC_BYTES == 16 + 2 * (8 * COLS + 8 * 8 * COLS)
+    planes = blob[16 + programs.REC_BYTES + 8 * COLS:].view(np.int32).reshape(8, COLS, 2)
+    assert planes[0, 6].tolist() == [5, np.float32(0.5).view(np.int32)]
+    assert planes[1, 6].tolist() == [6, np.float32(0.5).view(np.int32)]
+    assert planes[1, 7].tolist() == [0, 0] and not planes[2:].any()
+
+
+def test_program_too_many_terms_is_not_fused():
+    m = torch.zeros(1, 77, 77)
+    m[0, :9, 3] = 1.0 / 9
+    with pytest.raises(ValueError):
+        programs.replace_program(m).blob()
