@@ -10,6 +10,7 @@ reference-style controller, to the materialised protocol (attention.py).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -146,16 +147,54 @@ class DummyController:
         self.num_att_layers = 0
 
 
+FUSE_PROJECTIONS = os.environ.get("P2P_FUSE_QKV", "1") != "0"
+
+
+def _stacked_weight(module, names):
+    """One [sum(out), in] weight for the bias-free projections ``names`` of ``module``
+    (diffusers-0.8.1 CrossAttention's to_q/to_k/to_v carry no bias), rebuilt whenever a
+    source weight is replaced or modified in place; None when they cannot be stacked."""
+    mods = [getattr(module, n, None) for n in names]
+    if not all(type(m) is torch.nn.Linear and m.bias is None for m in mods):
+        return None
+    key = tuple((m.weight.data_ptr(), m.weight._version, m.weight.dtype) for m in mods)
+    cache = module.__dict__.setdefault("_p2p_stacked", {})
+    hit = cache.get(names)
+    if hit is None or hit[0] != key:
+        hit = (key, torch.cat([m.weight.detach() for m in mods]))
+        cache[names] = hit
+    return hit[1]
+
+
+def _project(module, x, context, is_cross):
+    """q, k, v of ptp_utils.py:186-193.  Outside autograd one GEMM produces them (x read once
+    for self-attention, the context once for k and v) and the kernels read q/k/v as strided
+    views of its output -- no head split copies (``[b,n,h*d] -> [b*h,n,d]``, :191-193)."""
+    src = context if is_cross else x
+    grad = torch.is_grad_enabled() and (x.requires_grad or src.requires_grad)
+    if FUSE_PROJECTIONS and not grad and x.is_cuda:
+        if is_cross:
+            w = _stacked_weight(module, ("to_k", "to_v"))
+            if w is not None:
+                kv = torch.nn.functional.linear(src, w)
+                C = kv.shape[-1] // 2
+                return module.to_q(x), kv[..., :C], kv[..., C:]
+        else:
+            w = _stacked_weight(module, ("to_q", "to_k", "to_v"))
+            if w is not None:
+                qkv = torch.nn.functional.linear(x, w)
+                C = qkv.shape[-1] // 3
+                return qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    return module.to_q(x), module.to_k(src), module.to_v(src)
+
+
 def _make_forward(module, place_in_unet, controller):
     to_out = module.to_out[0] if type(module.to_out) is torch.nn.modules.container.ModuleList else module.to_out
     attend = getattr(controller, "attention", None)
 
     def forward(x, context=None, mask=None, encoder_hidden_states=None, attention_mask=None):
-        q = module.to_q(x)
         is_cross = context is not None          # only the ``context=`` kwarg counts (:187)
-        src = context if is_cross else x
-        k = module.to_k(src)
-        v = module.to_v(src)
+        q, k, v = _project(module, x, context, is_cross)
         if attend is not None:
             out = attend(q, k, v, module.heads, module.scale, is_cross, place_in_unet, mask)
         else:

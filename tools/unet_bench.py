@@ -53,8 +53,11 @@ def run(channels_last, benchmark, graph, iters=20):
 
 
 if __name__ == "__main__":
-    for cl, bm, gr in ((False, False, False), (True, False, False), (True, True, False), (False, True, False),
-                       (True, True, True), (False, False, True)):
+    configs = ((False, False, False), (True, False, False), (True, True, False), (False, True, False),
+               (True, True, True), (False, False, True))
+    if "--quick" in sys.argv:
+        configs = configs[:1]
+    for cl, bm, gr in configs:
         ms, enq = run(cl, bm, gr)
-        print(f"unet bf16 channels_last={cl} benchmark={bm} graph={gr}: {ms:.2f} ms/call (enqueue {enq:.2f} ms)",
+        print(f"[P2P_FUSE_QKV={os.environ.get('P2P_FUSE_QKV', '1')}] unet bf16 channels_last={cl} benchmark={bm} graph={gr}: {ms:.2f} ms/call (enqueue {enq:.2f} ms)",
               flush=True)
