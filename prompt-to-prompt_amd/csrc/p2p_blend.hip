@@ -8,8 +8,8 @@
 //   mask   = (m / max_{y,x} m) > th;  mask = mask[:1] | mask
 //   mask  &= ~(substruct mask)               (optional, unpooled, th[1])
 //   x_t    = x_t[:1] + mask * (x_t - x_t[:1])
-// Kernel 1 reduces the word axis for every (prompt, layer x head) map; kernel 2 does the rest
-// for the whole prompt group in one workgroup (the mask of prompt 0 gates every other prompt).
+// Kernel 1 reduces the word axis for every (prompt, layer x head) map; kernel 2 does the rest,
+// one workgroup per prompt (each rebuilds prompt 0's mask, which gates every other prompt).
 #include "p2p_device.h"
 #include "p2p_kernels.h"
 
@@ -17,7 +17,11 @@ namespace p2p {
 
 constexpr int kBlendMaxPrompts = 16;
 
-// grid (n_prompts, n_maps * heads), block = res*res threads (one per pixel)
+// grid (n_prompts, n_maps * heads, pixel chunks of kWsPix), 256 threads.  A chunk's rows
+// [kWsPix, W] are one contiguous span of the store: the workgroup copies it to LDS with
+// coalesced 16-byte loads, then every thread sums one pixel's words in index order.
+constexpr int kWsPix = 64;
+
 __global__ __launch_bounds__(256) void blend_wordsum_kernel(p2p_blend_args a) {
   const int b = blockIdx.x;
   const int j = blockIdx.y;                 // l * heads + hd
@@ -25,24 +29,36 @@ __global__ __launch_bounds__(256) void blend_wordsum_kernel(p2p_blend_args a) {
   const int hd = j - l * a.heads_per_map;
   const int R2 = a.map_res * a.map_res;
   const int W = a.n_words;
+  const int p0 = blockIdx.z * kWsPix;
+  const int npix = min(kWsPix, R2 - p0);
   __shared__ float sa[128], ss[128];
+  __shared__ __attribute__((aligned(16))) float rows[kWsPix * 128];
   for (int w = threadIdx.x; w < W; w += blockDim.x) {
     sa[w] = a.alpha_layers[b * W + w];
     ss[w] = a.substruct_layers ? a.substruct_layers[b * W + w] : 0.f;
   }
+  const float* m = a.maps[l] + ((int64_t)(b * a.heads_per_map + hd) * R2 + p0) * W;
+  const int n = npix * W;
+  if ((((uintptr_t)m) & 15) == 0) {
+    for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
+      reinterpret_cast<f32x4_t*>(rows)[i] = reinterpret_cast<const f32x4_t*>(m)[i];
+    for (int i = (n & ~3) + threadIdx.x; i < n; i += blockDim.x) rows[i] = m[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) rows[i] = m[i];
+  }
   __syncthreads();
   const int pix = threadIdx.x;
-  if (pix >= R2) return;
-  const float* m = a.maps[l] + ((int64_t)(b * a.heads_per_map + hd) * R2 + pix) * W;
+  if (pix >= npix) return;
+  const float* r = rows + pix * W;          // W odd (77): the 64 rows hit distinct banks
   float acc_a = 0.f, acc_s = 0.f;
   for (int w = 0; w < W; ++w) {
-    const float v = m[w];
+    const float v = r[w];
     acc_a += v * sa[w];
     acc_s += v * ss[w];
   }
   const int LH = a.n_maps * a.heads_per_map;
-  a.word_sums[((int64_t)(b * 2 + 0) * LH + j) * R2 + pix] = acc_a;
-  a.word_sums[((int64_t)(b * 2 + 1) * LH + j) * R2 + pix] = acc_s;
+  a.word_sums[((int64_t)(b * 2 + 0) * LH + j) * R2 + p0 + pix] = acc_a;
+  a.word_sums[((int64_t)(b * 2 + 1) * LH + j) * R2 + p0 + pix] = acc_s;
 }
 
 // x0 + m * (xb - x0) rounded exactly as the reference's three tensor ops (no fma contraction)
@@ -53,87 +69,114 @@ __device__ __forceinline__ float blend1(float x0, float xb, float m) {
   return x0 + t;
 }
 
-// one workgroup for the whole prompt group
+// one workgroup per prompt b: it rebuilds the source prompt's pooled mask next to its own (the
+// source mask gates every prompt, mask = mask[:1] | mask), so the prompts run in parallel and no
+// workgroup reads another's output (x_t[0] is never written: x_t[0] + mask * 0 == x_t[0])
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
 __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
-  const int B = a.n_prompts;
+  const int b = blockIdx.x;
   const int R = a.map_res;
   const int R2 = R * R;
   const int LH = a.n_maps * a.heads_per_map;
   const int HW = a.lat_h * a.lat_w;
-  __shared__ float mean_a[kBlendMaxPrompts][256];
-  __shared__ float mean_s[kBlendMaxPrompts][256];
-  __shared__ float pooled[kBlendMaxPrompts][256];
-  __shared__ float vmax[kBlendMaxPrompts][2];
+  __shared__ float mean_a[2][256];   // [0] = source prompt, [1] = prompt b
+  __shared__ float mean_s[2][256];
+  __shared__ float pooled[2][256];
+  __shared__ float red[4][4];        // per-wave maxima: (pooled, substruct) x (source, b)
   const int tid = threadIdx.x;
   const bool sub = a.substruct_layers != nullptr;
 
   // mean over the L*H maps (sum in index order, then / L*H as Tensor.mean does)
-  for (int i = tid; i < B * R2; i += blockDim.x) {
-    const int b = i / R2, pix = i - b * R2;
+  for (int i = tid; i < 2 * R2; i += blockDim.x) {
+    const int k = i / R2, pix = i - k * R2;
+    const int bb = k ? b : 0;
+    const float* wa = a.word_sums + (int64_t)(bb * 2 + 0) * LH * R2 + pix;
+    const float* ws = a.word_sums + (int64_t)(bb * 2 + 1) * LH * R2 + pix;
     float sa = 0.f, ss = 0.f;
-    for (int j = 0; j < LH; ++j) {
-      sa += a.word_sums[((int64_t)(b * 2 + 0) * LH + j) * R2 + pix];
-      ss += a.word_sums[((int64_t)(b * 2 + 1) * LH + j) * R2 + pix];
+    for (int j0 = 0; j0 < LH; j0 += 16) {   // 32 loads in flight, then the in-order sums
+      float va[16], vs[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int j = min(j0 + u, LH - 1);
+        va[u] = wa[(int64_t)j * R2];
+        vs[u] = ws[(int64_t)j * R2];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (j0 + u < LH) {
+          sa += va[u];
+          ss += vs[u];
+        }
     }
-    mean_a[b][pix] = sa / (float)LH;
-    mean_s[b][pix] = ss / (float)LH;
+    mean_a[k][pix] = sa / (float)LH;
+    mean_s[k][pix] = ss / (float)LH;
   }
   __syncthreads();
   // 3x3 max-pool, stride 1, padding 1 (padding never wins: -inf)
-  for (int i = tid; i < B * R2; i += blockDim.x) {
-    const int b = i / R2, pix = i - b * R2;
+  for (int i = tid; i < 2 * R2; i += blockDim.x) {
+    const int k = i / R2, pix = i - k * R2;
     const int y = pix / R, x = pix - y * R;
     float m = -INFINITY;
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
         const int yy = y + dy, xx = x + dx;
-        if (yy >= 0 && yy < R && xx >= 0 && xx < R) m = fmaxf(m, mean_a[b][yy * R + xx]);
+        if (yy >= 0 && yy < R && xx >= 0 && xx < R) m = fmaxf(m, mean_a[k][yy * R + xx]);
       }
-    pooled[b][pix] = m;
+    pooled[k][pix] = m;
   }
   __syncthreads();
-  // per-image max of the nearest-upsampled maps: a block-wide max over the upsampled grid
+  // per-image max of the nearest-upsampled maps.  Upsampling (latent >= map resolution) samples
+  // every source pixel, so the max over the grid is the max over the R*R sources.
   const float sy = (float)R / (float)a.lat_h, sx = (float)R / (float)a.lat_w;
-  __shared__ float red[2][256];
-  for (int b = 0; b < B; ++b) {
-    float m0 = -INFINITY, m1 = -INFINITY;
-    for (int yx = tid; yx < HW; yx += blockDim.x) {
-      const int Y = yx / a.lat_w, X = yx - Y * a.lat_w;
-      const int src = min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
-      m0 = fmaxf(m0, pooled[b][src]);
-      m1 = fmaxf(m1, mean_s[b][src]);
-    }
-    red[0][tid] = m0;
-    red[1][tid] = m1;
-    __syncthreads();
-    for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
-      if (tid < s2) {
-        red[0][tid] = fmaxf(red[0][tid], red[0][tid + s2]);
-        red[1][tid] = fmaxf(red[1][tid], red[1][tid + s2]);
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      vmax[b][0] = red[0][0];
-      vmax[b][1] = red[1][0];
-    }
-    __syncthreads();
-  }
-  // masks + latent blend: x_t[b] = x_t[0] + mask * (x_t[b] - x_t[0])
-  for (int i = tid; i < B * HW; i += blockDim.x) {
-    const int b = i / HW, yx = i - b * HW;
+  auto src_of = [&](int yx) {
     const int Y = yx / a.lat_w, X = yx - Y * a.lat_w;
-    const int src = min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
-    bool m0 = pooled[0][src] / vmax[0][0] > a.th_pool;
-    bool mb = pooled[b][src] / vmax[b][0] > a.th_pool;
+    return min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
+  };
+  const bool all_sources = a.lat_h >= R && a.lat_w >= R;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int i = tid; i < (all_sources ? R2 : HW); i += blockDim.x) {
+    const int src = all_sources ? i : src_of(i);
+    m[0] = fmaxf(m[0], pooled[0][src]);
+    m[1] = fmaxf(m[1], mean_s[0][src]);
+    m[2] = fmaxf(m[2], pooled[1][src]);
+    m[3] = fmaxf(m[3], mean_s[1][src]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) m[c] = wave_max(m[c]);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[tid >> 6][c] = m[c];
+  __syncthreads();
+  float vmax[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    vmax[c] = red[0][c];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) vmax[c] = fmaxf(vmax[c], red[w][c]);
+  }
+  // mask of prompt b per source pixel (the thresholds of null_text.py:62-67), then gathered by
+  // the nearest upsampling: identical per output pixel, evaluated 256 times instead of H*W
+  __shared__ float msrc[256];
+  for (int pix = tid; pix < R2; pix += blockDim.x) {
+    const bool m0 = pooled[0][pix] / vmax[0] > a.th_pool;
+    const bool mb = pooled[1][pix] / vmax[2] > a.th_pool;
     bool mask = m0 || mb;
     if (sub) {
-      const bool s0 = mean_s[0][src] / vmax[0][1] > a.th_sub;
-      const bool sb = mean_s[b][src] / vmax[b][1] > a.th_sub;
+      const bool s0 = mean_s[0][pix] / vmax[1] > a.th_sub;
+      const bool sb = mean_s[1][pix] / vmax[3] > a.th_sub;
       mask = mask && !(s0 || sb);
     }
-    const float mf = mask ? 1.f : 0.f;
-    if (a.mask_out) a.mask_out[(int64_t)b * HW + yx] = mask ? 1 : 0;
+    msrc[pix] = mask ? 1.f : 0.f;
+  }
+  __syncthreads();
+  // x_t[b] = x_t[0] + mask * (x_t[b] - x_t[0])
+  for (int yx = tid; yx < HW; yx += blockDim.x) {
+    const float mf = msrc[src_of(yx)];
+    if (a.mask_out) a.mask_out[(int64_t)b * HW + yx] = mf != 0.f ? 1 : 0;
     if (b == 0 || !a.x_t) continue;  // x_t[0] + mask * 0 == x_t[0]; mask-only mode
     for (int ch = 0; ch < a.channels; ++ch) {
       const float x0 = a.x_t[(int64_t)(0 * a.channels + ch) * HW + yx];
@@ -237,9 +280,9 @@ int run_localblend(const p2p_blend_args& a, hipStream_t st) {
     return P2P_E_ARG;
   for (int l = 0; l < a.n_maps; ++l)
     if (!a.maps[l]) return P2P_E_ARG;
-  dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map);
+  dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map, (a.map_res * a.map_res + kWsPix - 1) / kWsPix);
   hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
-  hipLaunchKernelGGL(blend_finalize_kernel, dim3(1), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(blend_finalize_kernel, dim3(a.n_prompts), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
