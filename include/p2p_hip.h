@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 6
+#define P2P_ABI_VERSION 7
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -30,6 +30,9 @@ extern "C" {
 #define P2P_PROGRAM_TMAX 8   /* term planes per edit (source words per target word)  */
 /* bytes of one edit's record: c_rep f32[COLS] | post f32[COLS] | {i32 row, f32 val}[TMAX][COLS] */
 #define P2P_PROGRAM_REC_BYTES (2 * 4 * P2P_PROGRAM_COLS + 8 * P2P_PROGRAM_TMAX * P2P_PROGRAM_COLS)
+#define P2P_PROGRAM_HEADER_BYTES 32
+#define P2P_PROGRAM_DENSE 96 /* dense mapper tile: bf16 [DENSE][DENSE] per edit             */
+enum { P2P_PROGRAM_F_DENSE = 1 }; /* p2p_group.flags: the program carries the dense bf16 tile */
 
 enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };
 enum { P2P_COMPUTE_BF16 = 0, P2P_COMPUTE_F32 = 1 };
@@ -78,18 +81,25 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
  * entry `first` is the source prompt, the others its edits (main.py:187).  program is the
  * device edit program or NULL
  * for no edit; alpha is the device [count - 1][n_key] row cross_replace_alpha[cur_step]
- * (main.py:189).  Program layout (p2p_amd/programs.py): int32 header {n_edits, n_cols, tmax,
- * P2P_PROGRAM_COLS}, then per edit e at byte 16 + e * P2P_PROGRAM_REC_BYTES: c_rep f32[COLS],
+ * (main.py:189).  Program layout (p2p_amd/programs.py): int32 header[8] {n_edits, n_cols, tmax,
+ * P2P_PROGRAM_COLS, dense, dense_offset, 0, 0}, then per edit e at byte
+ * P2P_PROGRAM_HEADER_BYTES + e * P2P_PROGRAM_REC_BYTES: c_rep f32[COLS],
  * post f32[COLS], term planes {i32 row, f32 val}[P2P_PROGRAM_TMAX][COLS] -- plane t of column
  * w is the t-th source row feeding target word w, (0, 0.0) past its last term; tmax <= TMAX is
  * the number of planes the kernel walks:
  *   R[w] = post[w] * (c_rep[w] * P_e[w] + sum_{t < tmax} val[t][w] * P_0[row[t][w]])
- *   P_e'[w] = alpha[w] * R[w] + (1 - alpha[w]) * P_e[w]                                    */
+ *   P_e'[w] = alpha[w] * R[w] + (1 - alpha[w]) * P_e[w]
+ * When every term value is exact in bf16 the program also holds, at byte dense_offset, the
+ * dense mapper of each edit as bf16 [P2P_PROGRAM_DENSE rows (source word)][P2P_PROGRAM_DENSE
+ * cols (target word)] (zeros elsewhere), and the host sets P2P_PROGRAM_F_DENSE in flags: the
+ * bf16 kernels then form sum_t val * P_0[row] as the MFMA product P_0 . M_e (P_0 split into
+ * two bf16 parts, ~2^-16 relative) instead of an LDS gather.                                */
 typedef struct {
   int32_t first;
   int32_t count;
   const void* program;
   const float* alpha;
+  int32_t flags; /* P2P_PROGRAM_F_* of program (host-known: sizes the launch's LDS) */
 } p2p_group;
 
 /* Cross-attention (ptp_utils.py:183-208 with context=...) with the controller's cross edit

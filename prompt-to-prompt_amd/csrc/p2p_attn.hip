@@ -554,8 +554,8 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 // Stored maps leave through the same slab as whole contiguous rows (one [32, K] block per
 // wave).  The slab is dynamic LDS, allocated only by launches with an edit or a store, so a
 // plain launch runs at the occupancy of its K/V tiles alone.
-template <typename IO, typename MQ, typename MP, int D, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
+template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
+__global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
   constexpr int DK = (D + 15) / 16 * 16;
@@ -686,7 +686,63 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
 
   typename MQ::frag qf[NKT];
   float sv[KB][16];
-  if (edit) {
+  // dense edit (bf16 PV path, program carries the bf16 mapper tile): R = P0 . M_e on the MFMA
+  constexpr bool kDenseOk = DENSE && MP::kElemBytes == 2;  // separate instantiation: its VGPRs
+  constexpr int kDenseTile = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * 2;  // bytes of the bf16 tile
+  const bool dense = kDenseOk && edit;   // the launcher picks DENSE only if every edit group is
+  f32x16_t Rd[KB];
+  if constexpr (kDenseOk) {
+   if (dense) {
+    const int* hdr = reinterpret_cast<const int*>(prog);
+    const uint16_t* mg = reinterpret_cast<const uint16_t*>(prog + hdr[5]) +
+                         (int64_t)(b - 1) * P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE;
+    EV* const Ms = reinterpret_cast<EV*>(cross_dyn);  // [96 source words][96 target words]
+    load_q(first, qf);
+    for (int i = tid; i < P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE / 8; i += NT)
+      reinterpret_cast<short8_t*>(Ms)[i] = reinterpret_cast<const short8_t*>(mg)[i];
+    {  // per-column c_rep / post / alpha next to the tile, read back after the barriers
+      const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
+                                                       (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES);
+      const float* al = a.grp_alpha[gi] + (b - 1) * K;
+      float* col = reinterpret_cast<float*>(cross_dyn + kDenseTile);
+      for (int w = tid; w < KR; w += NT) {
+        col[w] = ce[w];
+        col[KR + w] = ce[P2P_PROGRAM_COLS + w];
+        col[2 * KR + w] = w < K ? al[w] : 0.f;
+      }
+    }
+    stage(first, false);
+    __syncthreads();
+    float p0[KB][16];
+    probs(qf, p0);
+    load_q(n, qf);
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) Rd[kb] = f32x16_t{};
+    // P0 = hi + lo (two bf16 parts, ~2^-16 relative): R = M^T hi + M^T lo, every mapper
+    // fragment read once for both products; one 32-key block at a time (the scheduler would
+    // otherwise hoist all 36 fragment reads: 256 VGPRs)
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float lo[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) lo[r] = p0[kb][8 * s2 + r] - bf2f(f2bf(p0[kb][8 * s2 + r]));
+        const MmaBf16::frag bh = MmaBf16::pack_p(p0[kb] + 8 * s2);
+        const MmaBf16::frag bl = MmaBf16::pack_p(lo);
+#pragma unroll
+        for (int dt = 0; dt < KB; ++dt) {
+          const MmaBf16::frag af =
+              vt_frag<P2P_PROGRAM_DENSE>(reinterpret_cast<const uint16_t*>(Ms), kb * 32, s2, dt * 32, lane);
+          MmaBf16::mma(Rd[dt], af, bh);
+          MmaBf16::mma(Rd[dt], af, bl);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with the source K tile and the mapper tile
+   }
+  }
+  if (edit && !dense) {
     // ---- source probabilities P0 for these rows -> this wave's LDS slab
     load_q(first, qf);
     stage(first, false);
@@ -701,17 +757,39 @@ __global__ __launch_bounds__(64 * WAVES) void cross_attn_kernel(CrossArgs a) {
         if (w < K) slab[qi * P0S + w] = sv[kb][r];
       }
     __syncthreads();  // slab written; every wave is done reading the source K tile
-  } else {
+  } else if (!edit) {
     load_q(n, qf);
   }
   stage(n, true);
   __syncthreads();
   probs(qf, sv);
 
-  if (edit) {
+  if (dense) {
+#pragma clang fp contract(off)
+    // a lane's columns come in runs of 4 (r & 3): one 16-byte LDS read per run and table;
+    // one 32-column block at a time (hoisting every read costs ~150 VGPRs)
+    const float* const col = reinterpret_cast<const float*>(cross_dyn + kDenseTile);
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int w0 = kb * 32 + 8 * g + 4 * hh;
+        const f32x4_t c4 = *reinterpret_cast<const f32x4_t*>(col + w0);
+        const f32x4_t p4 = *reinterpret_cast<const f32x4_t*>(col + KR + w0);
+        const f32x4_t a4 = *reinterpret_cast<const f32x4_t*>(col + 2 * KR + w0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float pb = sv[kb][r];
+          const float R = p4[j] * (c4[j] * pb + Rd[kb][r]);
+          sv[kb][r] = a4[j] * R + (1.f - a4[j]) * pb;   // columns >= K: a = 0, p stays 0
+        }
+      }
+    }
+  } else if (edit) {
 #pragma clang fp contract(off)
     const int tmax = reinterpret_cast<const int*>(prog)[2];
-    const char* const rec = prog + 16 + (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES;
+    const char* const rec = prog + P2P_PROGRAM_HEADER_BYTES + (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES;
     const float* const ce = reinterpret_cast<const float*>(rec);
     const float* const pe = ce + P2P_PROGRAM_COLS;
     const int2* const terms = reinterpret_cast<const int2*>(pe + P2P_PROGRAM_COLS);
@@ -860,9 +938,20 @@ static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
   // the slab holds a [32, K] f32 block per wave: stride K | 1 (odd, so the 32 rows of one
   // column hit distinct banks) for the edit gather, K for the store rows
   b.slab_stride = a.K | 1;
-  const size_t slab = a.slab ? (size_t)W * 32 * b.slab_stride * sizeof(float) : 0;
+  // the dense path (bf16 PV only) stages the mapper tile in the same dynamic region the slab
+  // uses later (the tile is dead before any store)
+  constexpr bool kDense = MP::kElemBytes == 2;
+  const bool dense = kDense && a.edit_dense && !a.edit_terms;
+  b.slab = (a.any_store || ((a.edit_terms || a.edit_dense) && !dense)) ? 1 : 0;
+  size_t dyn = b.slab ? (size_t)W * 32 * b.slab_stride * sizeof(float) : 0;
+  const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t) +
+                      3 * P2P_MAX_KEYS_CROSS * sizeof(float);
+  if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W>), grid, block, slab, st, b);
+  if (dense)
+    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
+  else
+    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false>), grid, block, dyn, st, b);
   return hipGetLastError();
 }
 

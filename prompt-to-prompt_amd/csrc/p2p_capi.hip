@@ -109,6 +109,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     a.grp_count[g] = G.count;
     a.grp_prog[g] = G.program;
     a.grp_alpha[g] = G.alpha;
+    a.grp_flags[g] = G.program ? G.flags : 0;
     for (int e = G.first; e < G.first + G.count; ++e) {
       if (a.ent_group[e] >= 0) return P2P_E_BATCH;  // groups overlap
       a.ent_group[e] = g;
@@ -123,9 +124,13 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
   }
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;
-  bool any_edit = false;
-  for (int g = 0; g < n_groups; ++g) any_edit |= groups[g].program != nullptr && groups[g].count > 1;
-  a.slab = (any_store || any_edit) ? 1 : 0;
+  a.any_store = any_store ? 1 : 0;
+  a.edit_terms = a.edit_dense = 0;
+  for (int g = 0; g < n_groups; ++g)
+    if (groups[g].program && groups[g].count > 1) {
+      if (groups[g].flags & P2P_PROGRAM_F_DENSE) a.edit_dense = 1;
+      else a.edit_terms = 1;
+    }
   return run_cross(a, t->io_dtype, t->compute, t->head_dim, (hipStream_t)stream);
 }
 

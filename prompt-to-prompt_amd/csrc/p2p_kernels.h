@@ -40,7 +40,10 @@ struct CrossArgs {
   int n_qtiles;
   float* store;
   int store_accumulate;
-  int slab;                      // some entry edits or stores: the launch allocates the LDS slab
+  int any_store;                 // some entry stores its maps
+  int edit_terms;                // some group edits through the term planes (LDS gather)
+  int edit_dense;                // some group carries the dense bf16 mapper tile
+  int slab;                      // launcher-filled: the launch allocates the LDS slab
   int slab_stride;               // launcher-filled
   int store_slot[P2P_MAX_BATCH];
   int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
@@ -48,6 +51,7 @@ struct CrossArgs {
   int grp_count[P2P_MAX_GROUPS];
   const void* grp_prog[P2P_MAX_GROUPS];
   const float* grp_alpha[P2P_MAX_GROUPS];
+  int grp_flags[P2P_MAX_GROUPS];
 };
 
 enum { MODE_FUSED_ = 0, MODE_STORE_ = 1, MODE_PROBS_ = 2, MODE_PV_ = 3 };

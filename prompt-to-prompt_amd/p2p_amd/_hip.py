@@ -27,7 +27,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class HipError(RuntimeError):
@@ -50,7 +50,7 @@ class AttnTensors(ctypes.Structure):
 
 class Group(ctypes.Structure):
     _fields_ = [("first", ctypes.c_int32), ("count", ctypes.c_int32),
-                ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p)]
+                ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p), ("flags", ctypes.c_int32)]
 
 
 class BlendArgs(ctypes.Structure):
@@ -202,6 +202,7 @@ def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, sto
         G[i].first, G[i].count = int(first), int(count)
         G[i].program = prog.data_ptr() if prog is not None else None
         G[i].alpha = alpha.data_ptr() if alpha is not None else None
+        G[i].flags = int(getattr(prog, "p2p_flags", 0)) if prog is not None else 0
     slots = _i32_array(store_slot) if store_slot is not None else None
     if store is not None:
         _require_cuda(store)

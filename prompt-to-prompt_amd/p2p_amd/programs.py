@@ -18,9 +18,11 @@ zero terms removed (exact for single-entry columns, which is every column the ma
 builders produce except multi-token source words).
 
 Blob layout (include/p2p_hip.h; COLS = 128 column stride, TMAX = 8 term planes):
-    header  int32[4] = n_edits, n_cols, tmax, COLS
-    per edit e, at byte 16 + e * REC_BYTES:
+    header  int32[8] = n_edits, n_cols, tmax, COLS, dense, dense_offset, 0, 0
+    per edit e, at byte 32 + e * REC_BYTES:
         c_rep f32[COLS] | post f32[COLS] | term {i32 row, f32 val}[TMAX][COLS]
+    dense (when every term value is exact in bf16), at byte dense_offset:
+        bf16 [n_edits][96 source words][96 target words] -- the mapper as an MFMA operand
 Plane t of column w holds the t-th term of that column, (0, 0.0) past its last one; the kernel
 walks the first ``tmax`` planes for every column (a wave-uniform loop of independent loads), and
 the padding adds +0.0 after the real terms, so the sums keep the sparse order exactly.
@@ -36,6 +38,9 @@ import torch
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
 REC_BYTES = 2 * 4 * PROGRAM_COLS + 8 * PROGRAM_TMAX * PROGRAM_COLS
+HEADER_BYTES = 32
+DENSE = 96
+F_DENSE = 1
 
 
 @dataclass
@@ -66,11 +71,35 @@ class EditProgram:
                 for t, (r, v) in enumerate(self.terms[e][w]):
                     planes[t, w, 0] = np.uint32(np.int32(r).view(np.uint32))
                     planes[t, w, 1] = np.float32(v).view(np.uint32)
-        header = np.array([E, n, tmax, PROGRAM_COLS], np.int32)
-        return np.concatenate([header.view(np.uint8), rec.view(np.uint8).ravel()])
+        dense = self.dense_bf16()
+        dense_off = HEADER_BYTES + E * REC_BYTES if dense is not None else 0
+        header = np.array([E, n, tmax, PROGRAM_COLS, int(dense is not None), dense_off, 0, 0], np.int32)
+        parts = [header.view(np.uint8), rec.view(np.uint8).ravel()]
+        if dense is not None:
+            parts.append(dense.view(np.uint8).ravel())
+        return np.concatenate(parts)
+
+    def dense_bf16(self) -> Optional[np.ndarray]:
+        """The mappers as bf16 [E, 96, 96] (row = source word, col = target word), or None when a
+        term value is not exactly representable in bf16 (the kernel then gathers in f32)."""
+        E, n = self.n_edits, self.n_cols
+        if n > DENSE:
+            return None
+        m = torch.zeros(E, DENSE, DENSE, dtype=torch.float32)
+        for e in range(E):
+            for w in range(n):
+                for (r, v) in self.terms[e][w]:
+                    m[e, r, w] = float(np.float32(v))
+        mb = m.to(torch.bfloat16)
+        if not torch.equal(mb.float(), m):
+            return None
+        return mb.view(torch.int16).numpy().view(np.uint16)
 
     def to_device(self, device) -> torch.Tensor:
-        return torch.from_numpy(self.blob().copy()).to(device)
+        blob = self.blob()
+        t = torch.from_numpy(blob.copy()).to(device)
+        t.p2p_flags = F_DENSE if int(blob[16:20].view(np.int32)[0]) else 0   # p2p_group.flags
+        return t
 
 
 def replace_program(mapper: torch.Tensor) -> EditProgram:

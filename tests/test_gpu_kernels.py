@@ -157,6 +157,48 @@ def test_cross_plain_groups(cuda, compute, tol, P):
     assert (o - ref_out(p, v, H)).abs().max().item() < o_tol(v, compute)
 
 
+@pytest.mark.parametrize("weight", [0.5, 1.0 / 3.0], ids=["dense", "terms"])
+@pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
+@pytest.mark.parametrize("geom", [(4096, 40), (1024, 80)], ids=["G1", "G2"])
+def test_cross_edit_paths(cuda, weight, compute, tol, geom):
+    """Both edit paths of the cross kernel against the materialised einsum (main.py:217-218):
+    a mapper whose weights are bf16 values (1, 1/2) carries the dense tile (bf16 kernels: R on
+    the MFMA), one with 1/3 weights does not (LDS term-plane gather); the f32 check mode always
+    gathers.  Group layout as the controllers launch it: [uncond | source, 3 edits], store on."""
+    from p2p_amd import programs
+    P, d = geom
+    B, H, K = 4, 8, 77
+    N = 2 * B
+    q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=6.0, seed=21)
+    scale = d ** -0.5
+    mapper = torch.zeros(B - 1, K, K)
+    mapper[:, torch.arange(K), torch.arange(K)] = 1.0
+    mapper[0, 3, 3] = mapper[0, 4, 3] = weight        # a 2-/3-token source word -> one target word
+    if weight < 0.5:
+        mapper[0, 5, 3] = weight
+    mapper[1, 7, 7], mapper[1, 7, 8] = 0.0, 1.0       # swapped columns
+    mapper[1, 8, 8], mapper[1, 8, 7] = 0.0, 1.0
+    prog_host = programs.replace_program(mapper)
+    assert (prog_host.dense_bf16() is not None) == (weight == 0.5)
+    prog = prog_host.to_device(cuda)
+    alpha = torch.ones(B - 1, K, device=cuda)
+    alpha[2, 10:20] = 0.0                             # word-time alpha 0: own probabilities
+    o = torch.empty_like(q)
+    store = torch.zeros(B * H, P, K, device=cuda)
+    groups = [(0, B, None, None), (B, B, prog, alpha)]
+    _hip.cross_attn(q, k, v, o, H, scale, groups, compute=compute, store=store,
+                    store_slot=[-1] * B + [i * H for i in range(B)])
+    p = ref_probs(q, k, H, scale)                     # [N, H, P, K]
+    cond = p[B:].clone()
+    base = cond[0]
+    R = torch.einsum("hpw,bwn->bhpn", base, mapper.to(cuda))
+    a = alpha[:, None, None, :]
+    cond[1:] = R * a + (1 - a) * cond[1:]
+    assert (store - cond.reshape(B * H, P, K)).abs().max().item() < tol
+    want = torch.cat([p[:B], cond])
+    assert (o - ref_out(want, v, H)).abs().max().item() < o_tol(v, compute)
+
+
 def test_key_mask_materialise(cuda):
     N, P, K, H, d = 2, 64, 77, 2, 16
     q, k, v = make_qkv(N, P, K, H, d, torch.float32, seed=17)

@@ -16,11 +16,12 @@ COLS = programs.PROGRAM_COLS
 def run_blob(blob: np.ndarray, P0: np.ndarray, Pb: np.ndarray, alpha: np.ndarray) -> np.ndarray:
     """Reference interpreter of the kernel's edit step (p2p_attn.hip cross_attn_kernel): every
     column walks the first tmax term planes."""
-    hdr = blob[:16].view(np.int32)
+    hdr = blob[:32].view(np.int32)
     E, n, tmax = int(hdr[0]), int(hdr[1]), int(hdr[2])
     out = Pb.copy()                                   # [E, H, P, n]
+    H0 = programs.HEADER_BYTES
     for e in range(E):
-        rec = blob[16 + e * programs.REC_BYTES:16 + (e + 1) * programs.REC_BYTES]
+        rec = blob[H0 + e * programs.REC_BYTES:H0 + (e + 1) * programs.REC_BYTES]
         crep = rec[:4 * COLS].view(np.float32)
         post = rec[4 * COLS:8 * COLS].view(np.float32)
         planes = rec[8 * COLS:].view(np.int32).reshape(programs.PROGRAM_TMAX, COLS, 2)
@@ -137,13 +138,29 @@ def test_program_blob_layout():
     m[1, 5, 6] = 0.5                                  # column 6 of edit 1 gathers two rows
     m[1, 6, 6] = 0.5
     blob = programs.replace_program(m).blob()
-    hdr = blob[:16].view(np.int32)
-    assert hdr.tolist() == [2, 77, 2, COLS]
-    assert blob.nbytes == 16 + 2 * programs.REC_BYTES == 16 + 2 * (8 * COLS + 8 * 8 * COLS)
-    planes = blob[16 + programs.REC_BYTES + 8 * COLS:].view(np.int32).reshape(8, COLS, 2)
+    hdr = blob[:32].view(np.int32)
+    dense_off = 32 + 2 * programs.REC_BYTES
+    assert hdr.tolist() == [2, 77, 2, COLS, 1, dense_off, 0, 0]
+    assert blob.nbytes == dense_off + 2 * 96 * 96 * 2
+    planes = blob[32 + programs.REC_BYTES + 8 * COLS:dense_off].view(np.int32).reshape(8, COLS, 2)
     assert planes[0, 6].tolist() == [5, np.float32(0.5).view(np.int32)]
     assert planes[1, 6].tolist() == [6, np.float32(0.5).view(np.int32)]
     assert planes[1, 7].tolist() == [0, 0] and not planes[2:].any()
+    dense = torch.from_numpy(blob[dense_off:].view(np.int16).copy()).view(torch.bfloat16).float().reshape(2, 96, 96)
+    want = torch.zeros(2, 96, 96)
+    want[:, :77, :77] = m
+    assert torch.equal(dense, want)
+
+
+def test_program_dense_only_when_exact_in_bf16():
+    m = torch.zeros(1, 77, 77)
+    m[0, torch.arange(77), torch.arange(77)] = 1
+    m[0, 3:6, 4] = 1.0 / 3                            # 1/3 is not a bf16 value
+    prog = programs.replace_program(m)
+    assert prog.dense_bf16() is None
+    blob = prog.blob()
+    assert blob[:32].view(np.int32)[4:6].tolist() == [0, 0]
+    assert blob.nbytes == 32 + programs.REC_BYTES
 
 
 def test_program_too_many_terms_is_not_fused():

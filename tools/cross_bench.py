@@ -38,6 +38,8 @@ def main(iters=50):
     tok = default_tokenizer()
     mapper = seq_aligner.get_replacement_mapper(pl.north_star_prompts(), tok)
     prog = programs.replace_program(mapper).to_device("cuda")
+    # zero-term program: P0 recomputed and parked in the slab, no gather (isolates the gather cost)
+    prog0 = programs.replace_program(torch.zeros_like(mapper)).to_device("cuda")
     alpha = torch.ones(B - 1, K, device="cuda")
     rows = []
     for name, P, d in GEOMS:
@@ -51,8 +53,10 @@ def main(iters=50):
         slots = [-1] * B + [i * H for i in range(B)]
         plain = [(0, B, None, None), (B, B, None, None)]
         edit = [(0, B, None, None), (B, B, prog, alpha)]
+        edit0 = [(0, B, None, None), (B, B, prog0, alpha)]
         r = {"geom": name, "P": P, "d": d}
-        for tag, grp, st in (("plain", plain, None), ("edit", edit, None), ("store", plain, store),
+        for tag, grp, st in (("plain", plain, None), ("edit", edit, None), ("edit_no_terms", edit0, None),
+                             ("store", plain, store),
                              ("edit+store", edit, store)):
             fn = lambda: _hip.cross_attn(q, k, v, o, H, d ** -0.5, grp, store=st,  # noqa: E731
                                          store_slot=slots if st is not None else None,
