@@ -10,6 +10,8 @@
 //
 // Both kernels follow the transposed-fragment convention of p2p_device.h: S^T = K Q^T and
 // O^T = V^T P^T, query on the lane.
+#include <type_traits>
+
 #include "p2p_device.h"
 #include "p2p_kernels.h"
 
@@ -464,7 +466,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
   // tile prefetch on every iteration
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // one K/V tile; the key mask exists only in the instantiation for a partial last tile (as a
+  // runtime branch the compiler if-converted it: ~100 extra VALU per tile on every tile)
+  auto tile = [&](int kt, auto masked) {
     const int buf = kt & 1;
     if (kt + 1 < ntiles) stage_load(kt + 1);
     float sv[NSB][16];
@@ -480,7 +484,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
     }
-    if ((kt + 1) * BK > K) {
+    if constexpr (decltype(masked)::value) {
 #pragma unroll
       for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
@@ -519,7 +523,10 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
     for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
     if (kt + 1 < ntiles) stage_write(buf ^ 1);
     __syncthreads();
-  }
+  };
+  const int nfull = K / BK;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
   float l;
   if constexpr (kOnes) l = __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
   else l = l_run + __shfl_xor(l_run, 32);
