@@ -1,0 +1,78 @@
+"""BASELINE.json configs[4] timing: null-text inversion (null_text.py:469-628: DDIM inversion with the
+conditional U-Net, then per DDIM step up to 10 Adam steps on the null embedding with gradients through
+every patched attention -- p2p_attn_fwd_lse / p2p_attn_bwd) followed by the P2P AttentionReplace edit
+with the per-step null embeddings, 512x512 (64x64 latent), synthetic bf16 SD-v1.4-shaped U-Net.
+Prints one JSON line per phase.  Usage: python tools/nulltext_bench.py [ddim_steps] [inner_steps]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prompt-to-prompt_amd"))
+import torch  # noqa: E402
+
+from p2p_amd import null_text, ptp_utils  # noqa: E402
+from p2p_amd import pipeline as pl  # noqa: E402
+
+
+class CountingUNet(torch.nn.Module):
+    def __init__(self, unet):
+        super().__init__()
+        self.inner = unet
+        self.calls = 0
+
+    def forward(self, *args, **kw):
+        self.calls += 1
+        return self.inner(*args, **kw)
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.inner, name)
+
+
+def main(steps=50, inner=10):
+    dev = torch.device("cuda")
+    model = pl.SyntheticStableDiffusion(device=dev, dtype=torch.bfloat16)
+    x0 = torch.randn(1, 4, 64, 64, generator=torch.Generator().manual_seed(7)).to(dev)
+    prompt = pl.SOURCE
+    # warm-up (kernels, allocator, hipBLASLt heuristics) on a 2-step inversion; the scheduler is
+    # shared, as in the reference, so the timed instance is built afterwards (its __init__ sets
+    # the 50-step grid)
+    null_text.NullInversion(model, num_ddim_steps=2).invert(x0, prompt, num_inner_steps=1)
+    torch.cuda.synchronize()
+    inv = null_text.NullInversion(model, num_ddim_steps=steps)
+    counter = CountingUNet(model.unet)
+    unet = model.unet
+    model.unet = counter
+    t0 = time.perf_counter()
+    _, x_T, embs = inv.invert(x0, prompt, num_inner_steps=inner, early_stop_epsilon=1e-5)
+    torch.cuda.synchronize()
+    t_inv = time.perf_counter() - t0
+    calls = counter.calls
+    model.unet = unet
+    print(json.dumps({"config": "configs[4] null-text inversion", "ddim_steps": steps, "max_inner_steps": inner,
+                      "seconds": round(t_inv, 3), "unet_calls": calls, "ms_per_unet_call": round(1e3 * t_inv / calls, 2),
+                      "unet_dtype": "bf16", "latent": "64x64"}), flush=True)
+    prompts = [prompt] + pl.EDITS[:1]
+    # warm-up of the edit's batch-4 U-Net shapes (MIOpen compiles kernels per new shape)
+    ptp_utils.text2image_ldm_stable(model, prompts, null_text.AttentionReplace(prompts, 2, 0.8, 0.4, device=dev),
+                                    num_inference_steps=2, latent=x_T, uncond_embeddings=embs[:2])
+    ctrl = null_text.AttentionReplace(prompts, steps, 0.8, 0.4, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lat, _ = ptp_utils.text2image_ldm_stable(model, prompts, ctrl, num_inference_steps=steps, latent=x_T,
+                                             uncond_embeddings=embs)
+    torch.cuda.synchronize()
+    t_edit = time.perf_counter() - t0
+    assert torch.isfinite(lat).all()
+    print(json.dumps({"config": "configs[4] P2P edit after inversion", "prompts": len(prompts), "ddim_steps": steps,
+                      "seconds": round(t_edit, 3)}), flush=True)
+    print(json.dumps({"config": "configs[4] total", "seconds": round(t_inv + t_edit, 3),
+                      "inversions_per_s": round(1.0 / (t_inv + t_edit), 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main(*(int(x) for x in sys.argv[1:3]))
