@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 7
+#define P2P_ABI_VERSION 8
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -132,12 +132,16 @@ int p2p_attn_fwd_lse(const p2p_attn_tensors* t, float* lse, p2p_stream_t stream)
 /* Backward of O = softmax(Q K^T * scale) V for the same tensors (t->o = the forward's O):
  *   dV = P^T dO,  dS = P o (dO V^T - rowsum(dO o O)),  dQ = scale dS K,  dK = scale dS^T Q.
  * dout and dq use q's layout (strides of t->q / t->o); dk, dv are packed [n_batch, n_key,
- * n_heads * head_dim] in io_dtype, or f32 when kv_f32 = 1 (then they must be zero-filled:
- * the key/value pass may split the queries over workgroups and add with f32 atomics).
- * delta: workspace [n_batch * n_heads, n_query] f32.  P is recomputed from lse; bf16 MFMA
- * operands, f32 accumulation. */
+ * n_heads * head_dim], written (not accumulated) in io_dtype, or in f32 when kv_f32 = 1.
+ * delta: workspace [n_batch * n_heads, n_query] f32.  workspace: p2p_attn_bwd_workspace(t)
+ * bytes (NULL when that is 0): when the key tiles alone would leave the chip idle (cross
+ * attention, small batches) the key/value pass splits the queries over workgroups, each split
+ * stores its partial dK/dV there and a reduction adds them in split order -- deterministic,
+ * no atomics.  P is recomputed from lse; bf16 MFMA operands, f32 accumulation. */
+int64_t p2p_attn_bwd_workspace(const p2p_attn_tensors* t);
 int p2p_attn_bwd(const p2p_attn_tensors* t, const void* dout, const float* lse, float* delta, void* dq,
-                 void* dk, void* dv, int32_t kv_f32, p2p_stream_t stream);
+                 void* dk, void* dv, int32_t kv_f32, void* workspace, int64_t workspace_bytes,
+                 p2p_stream_t stream);
 
 /* LocalBlend (null_text.py:41-70; main.py:35-52 is the B=2 special case) for one prompt
  * group: maps[l] are the running-sum cross maps of the five 16x16 layers

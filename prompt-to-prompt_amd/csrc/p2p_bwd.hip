@@ -11,8 +11,12 @@
 //                     accumulator as the B operand and K^T from a transposable LDS image;
 //   bwd_dkv_kernel -- one wave per 32 keys (key on the lane): S = Q K^T, dP = dO V^T, then
 //                     dV^T += dO^T P and dK^T += Q^T dS with P / dS as B operands.
-// Cross-attention (77 keys) has too few key tiles to fill the chip, so its key/value pass splits
-// the queries over workgroups and adds into f32 dK/dV with global atomics.
+// Cross-attention (77 keys) and small batches have too few key tiles to fill the chip, so the
+// key/value pass splits the queries over workgroups: each split stores its partial dK/dV (f32)
+// into a workspace and bwd_kv_reduce_kernel adds them in split order (deterministic; the f32
+// atomics this replaced serialised on the shared rows: 3-4x slower).
+#include <cstdlib>
+
 #include "p2p_device.h"
 #include "p2p_kernels.h"
 
@@ -191,8 +195,9 @@ __global__ __launch_bounds__(64 * WAVES) void bwd_dq_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------- dK / dV pass
-// WANT: 1 = dV, 2 = dK, 3 = both.  OUT: element type of dk/dv (IO, or float for atomics / f32 out)
-template <typename IO, typename OUT, int D, int T, int WAVES, int WANT, bool ATOMIC>
+// WANT: 1 = dV, 2 = dK, 3 = both.  OUT: element type of dk/dv (IO or float); with a query split
+// the partials go to the f32 workspace instead.
+template <typename IO, typename OUT, int D, int T, int WAVES, int WANT>
 __global__ __launch_bounds__(64 * WAVES) void bwd_dkv_kernel(BwdArgs a) {
   using St = TileStage<IO, D, T, 64 * WAVES>;
   constexpr int NKT = St::DK / 16;
@@ -295,41 +300,101 @@ __global__ __launch_bounds__(64 * WAVES) void bwd_dkv_kernel(BwdArgs a) {
     __syncthreads();
   }
   if (!krow) return;
-  auto emit = [&](void* base, int64_t bs, int64_t ld, const f32x16_t (&acc)[NDT], float mul) {
+  const int64_t C = (int64_t)a.H * D;
+  auto emit = [&](void* base, int64_t bs, int64_t ld, int which, const f32x16_t (&acc)[NDT], float mul) {
+    if (a.kv_split > 1) {                       // partial of this split -> workspace (f32)
+      float* dst = a.ws + (((int64_t)which * a.kv_split + split) * a.N + n) * a.K * C + (int64_t)key * C + h * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = dt * 32 + 8 * g + 4 * hh;
+          if (dd < D)
+            store4(dst + dd, acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul,
+                   acc[dt][4 * g + 3] * mul);
+        }
+      return;
+    }
     OUT* dst = static_cast<OUT*>(base) + (int64_t)n * bs + (int64_t)key * ld + h * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int dd = dt * 32 + 8 * g + 4 * hh;
-        if (dd < D) {
-          if constexpr (ATOMIC) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) atomicAdd(reinterpret_cast<float*>(dst) + dd + e, acc[dt][4 * g + e] * mul);
-          } else {
-            store4(dst + dd, acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul,
-                   acc[dt][4 * g + 3] * mul);
-          }
-        }
+        if (dd < D)
+          store4(dst + dd, acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul,
+                 acc[dt][4 * g + 3] * mul);
       }
   };
-  if constexpr (kDV) emit(a.dv, a.bsdv, a.lddv, dV, 1.f);
-  if constexpr (kDK) emit(a.dk, a.bsdk, a.lddk, dK, a.scale);
+  if constexpr (kDV) emit(a.dv, a.bsdv, a.lddv, 1, dV, 1.f);
+  if constexpr (kDK) emit(a.dk, a.bsdk, a.lddk, 0, dK, a.scale);
+}
+
+// dk / dv [N, K, C] = sum over the splits (in split order) of the workspace partials
+template <typename OUT>
+__global__ __launch_bounds__(256) void bwd_kv_reduce_kernel(BwdArgs a, int64_t n4) {
+  const int64_t plane = n4 * 4;                 // N * K * C
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      const float* src = a.ws + (int64_t)which * a.kv_split * plane + 4 * i;
+      f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
+      for (int sp = 1; sp < a.kv_split; ++sp) s += *reinterpret_cast<const f32x4_t*>(src + sp * plane);
+      OUT* dst = static_cast<OUT*>(which ? a.dv : a.dk) + 4 * i;
+      store4(dst, s[0], s[1], s[2], s[3]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------- launchers
-template <typename IO, typename OUT, int D, int T, int W, int WANT, bool AT>
+template <typename IO, typename OUT, int D, int T, int W, int WANT>
 static void launch_dkv(const BwdArgs& a, hipStream_t st) {
   BwdArgs b = a;
   b.n_tiles = (a.K + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_tiles * a.N * a.H * a.kv_split), block(64 * W);
-  hipLaunchKernelGGL((bwd_dkv_kernel<IO, OUT, D, T, W, WANT, AT>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((bwd_dkv_kernel<IO, OUT, D, T, W, WANT>), grid, block, 0, st, b);
+}
+
+constexpr int kBwdWaves = 4;
+template <int D>
+struct BwdTile {
+  static constexpr int T = D >= 128 ? 32 : 64;
+};
+
+// query split of the key/value pass: double while the key workgroups leave the chip idle
+static int kv_split_for(int N, int H, int P, int K, int T) {
+  const int key_wgs = (K + 32 * kBwdWaves - 1) / (32 * kBwdWaves) * N * H;
+  int split = 1;
+  while (key_wgs * split < 512 && split * 2 * T <= P) split *= 2;
+  return split;
+}
+
+int bwd_kv_split(int N, int H, int P, int K, int d) {
+  return kv_split_for(N, H, P, K, d >= 128 ? 32 : 64);
+}
+
+// d >= 128: dV and dK in two passes (each keeps 5 O^T tiles of accumulators, not 10)
+template <typename IO, typename OUT, int D, int T, int W>
+static void launch_kv_out(const BwdArgs& a, hipStream_t st) {
+  if constexpr (D >= 128) {
+    launch_dkv<IO, OUT, D, T, W, 1>(a, st);
+    launch_dkv<IO, OUT, D, T, W, 2>(a, st);
+  } else {
+    launch_dkv<IO, OUT, D, T, W, 3>(a, st);
+  }
+  if (a.kv_split > 1) {
+    const int64_t n4 = (int64_t)a.N * a.K * a.H * D / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL((bwd_kv_reduce_kernel<OUT>), dim3((unsigned)blocks), dim3(256), 0, st, a, n4);
+  }
 }
 
 template <typename IO, int D>
 static int launch_bwd_d(BwdArgs a, hipStream_t st) {
-  constexpr int T = D >= 128 ? 32 : 64;
-  constexpr int W = 4;
+  constexpr int T = BwdTile<D>::T;
+  constexpr int W = kBwdWaves;
   const int64_t nd = (int64_t)a.N * a.H * a.P;
   hipLaunchKernelGGL((bwd_delta_kernel<IO, D>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, a);
   {
@@ -337,37 +402,11 @@ static int launch_bwd_d(BwdArgs a, hipStream_t st) {
     b.n_tiles = (a.P + 32 * W - 1) / (32 * W);
     hipLaunchKernelGGL((bwd_dq_kernel<IO, D, T, W>), dim3(b.n_tiles * a.N * a.H), dim3(64 * W), 0, st, b);
   }
-  // key/value pass: split the queries when the key tiles alone leave the chip idle (cross attention)
-  const int key_wgs = (a.K + 32 * W - 1) / (32 * W) * a.N * a.H;
-  int split = 1;
-  while (key_wgs * split < 512 && split * 2 * T <= a.P) split *= 2;
-  if (split > 1 && !a.kv_f32) return P2P_E_ARG;   // atomics need the f32 dk/dv form
-  a.kv_split = split;
-  // d >= 128: dV and dK in two passes (each keeps 5 O^T tiles of accumulators, not 10)
-  if (a.kv_f32) {
-    if (split > 1) {
-      if constexpr (D >= 128) {
-        launch_dkv<IO, float, D, T, W, 1, true>(a, st);
-        launch_dkv<IO, float, D, T, W, 2, true>(a, st);
-      } else {
-        launch_dkv<IO, float, D, T, W, 3, true>(a, st);
-      }
-    } else {
-      if constexpr (D >= 128) {
-        launch_dkv<IO, float, D, T, W, 1, false>(a, st);
-        launch_dkv<IO, float, D, T, W, 2, false>(a, st);
-      } else {
-        launch_dkv<IO, float, D, T, W, 3, false>(a, st);
-      }
-    }
-  } else {
-    if constexpr (D >= 128) {
-      launch_dkv<IO, IO, D, T, W, 1, false>(a, st);
-      launch_dkv<IO, IO, D, T, W, 2, false>(a, st);
-    } else {
-      launch_dkv<IO, IO, D, T, W, 3, false>(a, st);
-    }
-  }
+  // key/value pass: split the queries when the key tiles alone leave the chip idle
+  a.kv_split = kv_split_for(a.N, a.H, a.P, a.K, T);
+  if (a.kv_split > 1 && !a.ws) return P2P_E_ARG;   // the caller sized the workspace with bwd_kv_split
+  if (a.kv_f32) launch_kv_out<IO, float, D, T, W>(a, st);
+  else launch_kv_out<IO, IO, D, T, W>(a, st);
   return (int)hipGetLastError();
 }
 

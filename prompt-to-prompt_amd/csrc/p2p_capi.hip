@@ -193,11 +193,22 @@ int p2p_attn_fwd_lse(const p2p_attn_tensors* t, float* lse, p2p_stream_t stream)
   return run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_FUSED_, (hipStream_t)stream);
 }
 
+int64_t p2p_attn_bwd_workspace(const p2p_attn_tensors* t) {
+  if (!t || t->n_batch < 1 || t->n_query < 1 || t->n_key < 1 || t->n_heads < 1 || t->head_dim < 1) return 0;
+  const int split = bwd_kv_split(t->n_batch, t->n_heads, t->n_query, t->n_key, t->head_dim);
+  if (split <= 1) return 0;
+  return (int64_t)2 * split * t->n_batch * t->n_key * t->n_heads * t->head_dim * (int64_t)sizeof(float);
+}
+
 int p2p_attn_bwd(const p2p_attn_tensors* t, const void* dout, const float* lse, float* delta, void* dq,
-                 void* dk, void* dv, int32_t kv_f32, p2p_stream_t stream) {
+                 void* dk, void* dv, int32_t kv_f32, void* workspace, int64_t workspace_bytes,
+                 p2p_stream_t stream) {
   int rc = check_tensors(t, true, true, true, true);
   if (rc) return rc;
   if (!dout || !lse || !delta || !dq || !dk || !dv) return P2P_E_ARG;
+  const int64_t need = p2p_attn_bwd_workspace(t);
+  if (need > 0 && (!workspace || workspace_bytes < need)) return P2P_E_ARG;
+  if (need > 0 && !aligned16(workspace)) return P2P_E_ALIGN;
   if (t->compute != P2P_COMPUTE_BF16) return P2P_E_DTYPE;
   if (!aligned16(dout) || !aligned16(dq) || !aligned16(dk) || !aligned16(dv)) return P2P_E_ALIGN;
   BwdArgs a;
@@ -217,6 +228,7 @@ int p2p_attn_bwd(const p2p_attn_tensors* t, const void* dout, const float* lse, 
   a.n_tiles = 0;
   a.kv_split = 1;
   a.kv_f32 = kv_f32 ? 1 : 0;
+  a.ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
   return run_attn_bwd(a, t->io_dtype, t->head_dim, (hipStream_t)stream);
 }
 

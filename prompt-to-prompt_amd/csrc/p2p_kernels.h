@@ -72,10 +72,12 @@ struct BwdArgs {
   int N, P, K, H;
   float scale, scale_log2;
   int n_tiles;                 // launcher-filled
-  int kv_split;                // query splits of the dK/dV pass (>1: f32 atomics into dk/dv)
-  int kv_f32;                  // dk/dv are f32 buffers (atomic or not)
+  int kv_split;                // query splits of the dK/dV pass (>1: partials in ws, then a reduction)
+  int kv_f32;                  // dk/dv are f32 buffers
+  float* ws;                   // [2 (dK, dV)][kv_split][N][K][H*D] f32 partials when kv_split > 1
 };
 int run_attn_bwd(const BwdArgs& a, int io_dtype, int d, hipStream_t st);
+int bwd_kv_split(int N, int H, int P, int K, int d);   // launcher's query split (workspace sizing)
 int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
 
 }  // namespace p2p

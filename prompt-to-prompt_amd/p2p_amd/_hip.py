@@ -27,7 +27,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class HipError(RuntimeError):
@@ -98,7 +98,9 @@ def lib():
         L.p2p_store_scale.argtypes = [vp, vp, f32, i64, vp]
         L.p2p_latent_step.argtypes = [ctypes.POINTER(LatentArgs), vp]
         L.p2p_attn_fwd_lse.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
-        L.p2p_attn_bwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, vp, vp, vp, i32, vp]
+        L.p2p_attn_bwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, vp, vp, vp, i32, vp, i64, vp]
+        L.p2p_attn_bwd_workspace.argtypes = [ctypes.POINTER(AttnTensors)]
+        L.p2p_attn_bwd_workspace.restype = ctypes.c_int64
         for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
                    "p2p_localblend", "p2p_store_scale", "p2p_latent_step", "p2p_attn_fwd_lse", "p2p_attn_bwd"):
             getattr(L, fn).restype = ctypes.c_int
@@ -110,7 +112,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
                     "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step",
-                    "p2p_attn_fwd_lse", "p2p_attn_bwd")
+                    "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace")
 
 
 def _check(rc: int, what: str):
@@ -320,14 +322,21 @@ def attn_fwd_lse(q, k, v, o, heads, scale, lse):
     _check(lib().p2p_attn_fwd_lse(ctypes.byref(t), lse.data_ptr(), _stream(q.device)), "p2p_attn_fwd_lse")
 
 
-def attn_bwd(q, k, v, o, dout, lse, heads, scale, dq, dk, dv, delta):
-    """dq (q's dtype and layout), dk / dv f32 packed [N, K, H*d] (zero-filled: accumulated)."""
+def attn_bwd(q, k, v, o, dout, lse, heads, scale, dq, dk, dv, delta, workspace=None):
+    """dq (q's dtype and layout); dk / dv packed [N, K, H*d], written, in k's dtype or f32.
+    workspace: p2p_attn_bwd_workspace bytes (allocated here when None)."""
     for x in (q, k, v, o, dout, dq, dk, dv):
         assert x.is_contiguous()
     assert dout.shape == o.shape == q.shape and dq.shape == q.shape
-    assert dk.dtype == torch.float32 and dv.dtype == torch.float32 and dk.shape == k.shape and dv.shape == v.shape
+    assert dk.shape == k.shape and dv.shape == v.shape and dk.dtype == dv.dtype
+    assert dk.dtype in (k.dtype, torch.float32)
     t = make_tensors(q, k, v, o, heads, scale, "bf16")
     _require_cuda(dout, lse, delta, dq, dk, dv)
+    need = int(lib().p2p_attn_bwd_workspace(ctypes.byref(t)))
+    if need > 0 and (workspace is None or workspace.numel() * workspace.element_size() < need):
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    ws_ptr = workspace.data_ptr() if need > 0 else None
+    kv_f32 = int(dk.dtype == torch.float32)
     rc = lib().p2p_attn_bwd(ctypes.byref(t), dout.data_ptr(), lse.data_ptr(), delta.data_ptr(), dq.data_ptr(),
-                            dk.data_ptr(), dv.data_ptr(), 1, _stream(q.device))
+                            dk.data_ptr(), dv.data_ptr(), kv_f32, ws_ptr, need, _stream(q.device))
     _check(rc, "p2p_attn_bwd")

@@ -37,11 +37,11 @@ class _AttentionFn(torch.autograd.Function):
         q, k, v, o, lse = ctx.saved_tensors
         dout = dout.contiguous().to(q.dtype)
         dq = torch.empty_like(q)
-        dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
-        dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+        dk = torch.empty_like(k)                 # written by the kernels (f32 accumulation inside)
+        dv = torch.empty_like(v)
         delta = torch.empty_like(lse)
         _hip.attn_bwd(q, k, v, o, dout, lse, ctx.heads, ctx.scale, dq, dk, dv, delta)
-        return dq, dk.to(k.dtype), dv.to(v.dtype), None, None
+        return dq, dk, dv, None, None
 
 
 def differentiable_attention(q, k, v, heads, scale):

@@ -2,7 +2,7 @@
 conditional U-Net, then per DDIM step up to 10 Adam steps on the null embedding with gradients through
 every patched attention -- p2p_attn_fwd_lse / p2p_attn_bwd) followed by the P2P AttentionReplace edit
 with the per-step null embeddings, 512x512 (64x64 latent), synthetic bf16 SD-v1.4-shaped U-Net.
-Prints one JSON line per phase.  Usage: python tools/nulltext_bench.py [ddim_steps] [inner_steps]"""
+Prints one JSON line per phase.  Usage: python tools/nulltext_bench.py [ddim_steps] [inner_steps] [conv 0 = MIOpen immediate | 1 = MIOpen find | 2 = no MIOpen]"""
 import json
 import os
 import sys
@@ -33,7 +33,12 @@ class CountingUNet(torch.nn.Module):
             return getattr(self.inner, name)
 
 
-def main(steps=50, inner=10):
+def main(steps=50, inner=10, find=0):
+    # MIOpen immediate mode picks its naive convolution fallback for several batch-1/2 bf16 U-Net
+    # shapes (43-63 ms per call, rocprof); find mode (cudnn.benchmark) searches real kernels once
+    # (find = 2: bypass MIOpen -- PyTorch's own im2col + GEMM convolutions)
+    torch.backends.cudnn.benchmark = find == 1
+    torch.backends.cudnn.enabled = find != 2
     dev = torch.device("cuda")
     model = pl.SyntheticStableDiffusion(device=dev, dtype=torch.bfloat16)
     x0 = torch.randn(1, 4, 64, 64, generator=torch.Generator().manual_seed(7)).to(dev)
@@ -70,9 +75,9 @@ def main(steps=50, inner=10):
     assert torch.isfinite(lat).all()
     print(json.dumps({"config": "configs[4] P2P edit after inversion", "prompts": len(prompts), "ddim_steps": steps,
                       "seconds": round(t_edit, 3)}), flush=True)
-    print(json.dumps({"config": "configs[4] total", "seconds": round(t_inv + t_edit, 3),
+    print(json.dumps({"config": "configs[4] total", "conv_mode": ["miopen immediate", "miopen find", "torch im2col+gemm"][find], "seconds": round(t_inv + t_edit, 3),
                       "inversions_per_s": round(1.0 / (t_inv + t_edit), 4)}), flush=True)
 
 
 if __name__ == "__main__":
-    main(*(int(x) for x in sys.argv[1:3]))
+    main(*(int(x) for x in sys.argv[1:4]))
