@@ -216,11 +216,13 @@ class NullInversion:
     latent itself ([1, 4, H/8, W/8], the form the reference's ``image2latent`` passes through):
     the synthetic pipeline has no VAE."""
 
-    def __init__(self, model, num_ddim_steps: int = NUM_DDIM_STEPS, guidance_scale: float = GUIDANCE_SCALE):
+    def __init__(self, model, num_ddim_steps: int = NUM_DDIM_STEPS, guidance_scale: float = GUIDANCE_SCALE,
+                 use_graphs: bool = True):
         self.model = model
         self.tokenizer = model.tokenizer
         self.num_ddim_steps = num_ddim_steps
         self.guidance_scale = guidance_scale
+        self.use_graphs = use_graphs
         self.model.scheduler.set_timesteps(num_ddim_steps)
         self.prompt = None
         self.context = None
@@ -297,6 +299,8 @@ class NullInversion:
 
     def null_optimization(self, latents, num_inner_steps, epsilon):
         import torch.nn.functional as F
+        if self.use_graphs and latents[-1].is_cuda and hasattr(self.scheduler, "prev_coeffs"):
+            return self._null_optimization_graphed(latents, num_inner_steps, epsilon)
         uncond, cond = self.context.chunk(2)
         per_step = []
         latent_cur = latents[-1]
@@ -321,6 +325,40 @@ class NullInversion:
                 latent_cur = self.get_noise_pred(latent_cur, t, False, torch.cat([uncond, cond]))
         return per_step
 
+    def _null_optimization_graphed(self, latents, num_inner_steps, epsilon):
+        """null_optimization with each inner step (null_text.py:587-598: U-Net forward with the null
+        embedding as the only leaf, guided DDIM step, MSE, backward, Adam update) replayed from one
+        captured HIP graph.  The batch-1 step is host-bound eagerly (~40 ms of Python/launch work
+        for ~1500 kernels); the graph is captured once per inversion, and per DDIM step only its
+        inputs, the parameter, the Adam state and the learning rate are refilled in place.  The
+        early stop (null_text.py:597) still reads the loss after every step, as the reference."""
+        uncond, cond = self.context.chunk(2)
+        unet = self.model.unet
+        t0 = self.scheduler.timesteps[0]
+        step = _GraphedNullStep(self, latents[-1], uncond)
+        fwd_c = _GraphedForward(unet, latents[-1], cond, t0)                               # eps_c
+        fwd_cfg = _GraphedForward(unet, torch.cat([latents[-1]] * 2), torch.cat([uncond, cond]), t0)
+        per_step = []
+        self.inner_steps_run = 0
+        latent_cur = latents[-1]
+        for i in range(self.num_ddim_steps):
+            latent_prev = latents[len(latents) - i - 2]
+            t = self.scheduler.timesteps[i]
+            eps_c = fwd_c(latent_cur, t, cond)
+            step.reset(uncond, 1e-2 * (1.0 - i / 100.0), latent_cur, eps_c, latent_prev, t)
+            for _ in range(num_inner_steps):
+                step.graph.replay()
+                self.inner_steps_run += 1
+                if step.loss.item() < epsilon + i * 2e-5:
+                    break
+            uncond = step.param.detach().clone()
+            per_step.append(uncond[:1])
+            with torch.no_grad():                       # get_noise_pred(is_forward=False), graphed U-Net
+                eps = fwd_cfg(torch.cat([latent_cur] * 2), t, torch.cat([uncond, cond]))
+                eps_u, eps_cc = eps.chunk(2)
+                latent_cur = self.prev_step(eps_u + self.guidance_scale * (eps_cc - eps_u), t, latent_cur)
+        return per_step
+
     def invert(self, image, prompt: str, offsets=(0, 0, 0, 0), num_inner_steps=10, early_stop_epsilon=1e-5,
                verbose=False):
         from . import ptp_utils
@@ -334,3 +372,97 @@ class NullInversion:
             print("Null-text optimization...")
         uncond_embeddings = self.null_optimization(ddim_latents, num_inner_steps, early_stop_epsilon)
         return (image_gt, image_rec), ddim_latents[-1], uncond_embeddings
+
+
+class _GraphedForward:
+    """A no-grad U-Net call on fixed shapes captured as a HIP graph; __call__ refills the static
+    latent / timestep / context and replays (the output tensor is reused by the next replay)."""
+
+    def __init__(self, unet, x, ctx, t):
+        dev = x.device
+        self.x = x.detach().clone()
+        self.ctx = ctx.detach().clone()
+        self.t = torch.full((1,), int(t), dtype=torch.int64, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad():
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    unet(self.x, self.t, encoder_hidden_states=self.ctx)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = unet(self.x, self.t, encoder_hidden_states=self.ctx)["sample"]
+
+    @torch.no_grad()
+    def __call__(self, x, t, ctx):
+        self.x.copy_(x)
+        self.ctx.copy_(ctx)
+        self.t.fill_(int(t))
+        self.graph.replay()
+        return self.out
+
+
+class _GraphedNullStep:
+    """One null-text Adam step captured as a HIP graph (NullInversion._null_optimization_graphed).
+    Static inputs: the latent, eps_c, the target latent, the timestep and the four DDIM
+    coefficients of prev_step (ddim.DDIMScheduler.prev_coeffs: sqrt(1 - a_t), sqrt(a_t),
+    sqrt(a_prev), sqrt(1 - a_prev)); the parameter and the capturable Adam state are updated in
+    place by every replay."""
+
+    def __init__(self, inv, latent, uncond):
+        import torch.nn.functional as F
+        dev = latent.device
+        self.inv = inv
+        self.x = latent.detach().clone()
+        self.eps_c = torch.zeros_like(self.x)
+        self.target = torch.zeros_like(self.x)
+        self.t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.coef = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.param = uncond.detach().clone().requires_grad_(True)
+        self.lr = torch.tensor(1e-2, dtype=torch.float32, device=dev)
+        self.opt = torch.optim.Adam([self.param], lr=self.lr, capturable=True)
+        g = inv.guidance_scale
+        unet = inv.model.unet
+
+        def body():
+            self.opt.zero_grad(set_to_none=False)
+            eps_u = unet(self.x, self.t, encoder_hidden_states=self.param)["sample"]
+            eps = eps_u + g * (self.eps_c - eps_u)
+            x0 = (self.x - self.coef[0] * eps) / self.coef[1]
+            prev = self.coef[2] * x0 + self.coef[3] * eps
+            loss = F.mse_loss(prev, self.target)
+            loss.backward()
+            self.opt.step()
+            return loss
+
+        # warm-up on a side stream (autograd buffers, Adam state, allocator), then capture
+        self.t.fill_(int(inv.scheduler.timesteps[0]))
+        self.coef.copy_(self._coeffs(inv.scheduler.timesteps[0]))
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = body()
+
+    def _coeffs(self, t):
+        c = self.inv.scheduler.prev_coeffs(t)        # (sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_1m_alpha_prev)
+        return torch.tensor([float(x) for x in c], dtype=torch.float32)
+
+    @torch.no_grad()
+    def reset(self, uncond, lr, latent, eps_c, target, t):
+        """A fresh Adam on a fresh copy of the null embedding (null_text.py:582-584)."""
+        self.param.copy_(uncond)
+        for st in self.opt.state.values():
+            for key in ("step", "exp_avg", "exp_avg_sq"):
+                st[key].zero_()
+        self.lr.fill_(lr)
+        self.x.copy_(latent)
+        self.eps_c.copy_(eps_c)
+        self.target.copy_(target)
+        self.t.fill_(int(t))
+        self.coef.copy_(self._coeffs(t))

@@ -26,12 +26,15 @@ def cos(a, b):
     return torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
 
 
-def test_null_text_inversion_matches_oracle(cuda):
+@pytest.mark.parametrize("use_graphs", [True, False], ids=["graphed", "eager"])
+def test_null_text_inversion_matches_oracle(cuda, use_graphs):
+    """graphed: every inner Adam step replayed from one captured HIP graph (the default);
+    eager: the reference's loop as written."""
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
     g = torch.Generator().manual_seed(5)
     x0 = torch.randn(1, 4, 64, 64, generator=g).to(cuda)
     with config.compute_mode("bf16"):
-        inv = null_text.NullInversion(model, num_ddim_steps=STEPS)
+        inv = null_text.NullInversion(model, num_ddim_steps=STEPS, use_graphs=use_graphs)
         (_, rec), x_T, embs = inv.invert(x0, PROMPT, num_inner_steps=INNER, early_stop_epsilon=1e-5)
         prod_traj = inv.ddim_loop(x0)
     assert rec is None and len(embs) == STEPS and all(e.shape == (1, 77, 768) for e in embs)

@@ -58,9 +58,10 @@ def main(steps=50, inner=10, find=0):
     t_inv = time.perf_counter() - t0
     calls = counter.calls
     model.unet = unet
+    inner_run = getattr(inv, "inner_steps_run", None)
     print(json.dumps({"config": "configs[4] null-text inversion", "ddim_steps": steps, "max_inner_steps": inner,
-                      "seconds": round(t_inv, 3), "unet_calls": calls, "ms_per_unet_call": round(1e3 * t_inv / calls, 2),
-                      "unet_dtype": "bf16", "latent": "64x64"}), flush=True)
+                      "graphs": inv.use_graphs, "seconds": round(t_inv, 3), "eager_unet_calls": calls,
+                      "adam_steps": inner_run, "unet_dtype": "bf16", "latent": "64x64"}), flush=True)
     prompts = [prompt] + pl.EDITS[:1]
     # warm-up of the edit's batch-4 U-Net shapes (MIOpen compiles kernels per new shape)
     ptp_utils.text2image_ldm_stable(model, prompts, null_text.AttentionReplace(prompts, 2, 0.8, 0.4, device=dev),
