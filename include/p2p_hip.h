@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 8
+#define P2P_ABI_VERSION 9
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -73,9 +73,13 @@ typedef struct {
  * values.  store (nullable) receives the normalised probabilities of every entry whose
  * store_slot (host) is >= 0 at maps [store_slot[n] + head] of a [*, n_query, n_key] f32
  * tensor, overwritten (store_accumulate = 0, first step) or added (= 1): the running sum
- * of AttentionStore.between_steps (main.py:135-142). */
+ * of AttentionStore.between_steps (main.py:135-142).  lse_workspace: f32
+ * [n_batch * n_heads, n_query] scratch, required (16-byte aligned) when some entry stores its
+ * maps, else ignored: the fused pass leaves each row's log-sum-exp there and the map pass
+ * recomputes the probabilities from it. */
 int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store,
-                      const int32_t* store_slot, int32_t store_accumulate, p2p_stream_t stream);
+                      const int32_t* store_slot, int32_t store_accumulate, float* lse_workspace,
+                      p2p_stream_t stream);
 
 /* A prompt group of a cross-attention launch: entries [first, first + count) of the batch;
  * entry `first` is the source prompt, the others its edits (main.py:187).  program is the

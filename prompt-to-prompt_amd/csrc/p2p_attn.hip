@@ -1,9 +1,11 @@
 // Fused Prompt-to-Prompt attention kernels for MI355X (gfx950).
 //
-// self_attn_kernel  : flash-style self-attention (ptp_utils.py:183-208, context=None) with the
-//                     source-map injection of AttentionControlEdit.replace_self_attention
-//                     (main.py:169-174 / null_text.py:224-230) as a batch index remap, and the
-//                     AttentionStore epilogue (main.py:129-142) for layers whose maps are kept.
+// self_attn_fused_kernel : flash-style self-attention (ptp_utils.py:183-208, context=None) with
+//                     the source-map injection of AttentionControlEdit.replace_self_attention
+//                     (main.py:169-174 / null_text.py:224-230) as a batch index remap.
+// self_maps_kernel  : the AttentionStore epilogue (main.py:129-142) for self layers whose maps
+//                     are kept, from the fused kernel's row log-sum-exp.
+// self_attn_kernel  : the materialise protocol (probabilities to HBM, then P V).
 // cross_attn_kernel : cross-attention over the 77 text tokens with the P2P cross edit
 //                     (AttentionControlEdit.forward, main.py:180-197) applied in registers
 //                     between the exact softmax and PV, for every prompt group.
@@ -34,11 +36,10 @@ template <>
 __device__ __forceinline__ uint16_t one_elem<uint16_t>() { return 0x3F80; }  // bf16 1.0
 
 // ====================================================================== self attention
-// MODE_FUSED : one online-softmax pass, O = softmax(S) V                        (no map kept)
-// MODE_STORE : pass 1 row max/sum, pass 2 exact P -> store + PV                 (maps kept)
-// MODE_PROBS : pass 1 + pass 2 writing P only                                   (materialise)
-// MODE_PV    : O = P V with P read from HBM                                     (materialise)
-enum { MODE_FUSED = 0, MODE_STORE = 1, MODE_PROBS = 2, MODE_PV = 3 };
+// The materialise protocol's two kernels (the fused path is self_attn_fused_kernel below):
+// MODE_PROBS : pass 1 row max/sum, pass 2 exact P written to HBM
+// MODE_PV    : O = P V with P read from HBM
+enum { MODE_FUSED = 0, MODE_PROBS = 2, MODE_PV = 3 };
 
 template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, int MODE>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
   constexpr int CPR = D / 8;
   constexpr int NCH = (BK * CPR + NT - 1) / NT;
   constexpr bool kNeedK = MODE != MODE_PV;
-  constexpr bool kNeedV = MODE == MODE_FUSED || MODE == MODE_STORE || MODE == MODE_PV;
+  constexpr bool kNeedV = MODE == MODE_PV;
   constexpr int KPLANE = BK * KS;                       // elements per K plane
   constexpr int KBUF = kNeedK ? KPLANE * MQ::planes : 0;  // elements per K buffer
   constexpr int VBUF = kNeedV ? BK * VS : 0;
@@ -164,52 +165,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
 
   float m_run = -INFINITY, l_run = 0.f;
 
-  if constexpr (MODE == MODE_FUSED) {
-    __syncthreads();
-    stage_load(0, true, true);
-    stage_write(0, true, true);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < ntiles) stage_load(kt + 1, true, true);
-      float sv[NSB][16];
-      scores(buf, kt, sv);
-      float mx = -INFINITY;
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mnew = fmaxf(m_run, mx * c);
-      const float alpha = fast_exp2(m_run - mnew);
-      float ls = 0.f;
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(fmaf(sv[sb][r], c, -mnew));
-          sv[sb][r] = e;
-          ls += e;
-        }
-      l_run = fmaf(l_run, alpha, ls);
-      m_run = mnew;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
-      const EV* Vb = Vs + buf * VBUF;
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
-      if (kt + 1 < ntiles) stage_write(buf ^ 1, true, true);
-      __syncthreads();
-    }
-    const float l = l_run + __shfl_xor(l_run, 32);
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) O[dt][r] *= inv;
-  } else if constexpr (MODE == MODE_STORE || MODE == MODE_PROBS) {
+  if constexpr (MODE == MODE_PROBS) {
     // ---- pass 1: exact row max and row sum
     __syncthreads();
     stage_load(0, true, false);
@@ -238,19 +194,18 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
       __syncthreads();
     }
     const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
-    // ---- pass 2: exact probabilities -> store (+ PV)
-    constexpr bool kPV = MODE == MODE_STORE;
+    // ---- pass 2: exact probabilities -> HBM
     const int slot = a.store_slot[n];
     float* const mp = (a.store && slot >= 0 && prow)
                           ? a.store + ((int64_t)(slot + h) * a.P + p) * (int64_t)K
                           : nullptr;
     const bool vec4 = (K & 3) == 0;
-    stage_load(0, true, kPV);
-    stage_write(0, true, kPV);
+    stage_load(0, true, false);
+    stage_write(0, true, false);
     __syncthreads();
     for (int kt = 0; kt < ntiles; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < ntiles) stage_load(kt + 1, true, kPV);
+      if (kt + 1 < ntiles) stage_load(kt + 1, true, false);
       float sv[NSB][16];
       scores(buf, kt, sv);
 #pragma unroll
@@ -280,12 +235,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
             }
           }
       }
-      if constexpr (kPV) {
-        const EV* Vb = Vs + buf * VBUF;
-#pragma unroll
-        for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
-      }
-      if (kt + 1 < ntiles) stage_write(buf ^ 1, true, kPV);
+      if (kt + 1 < ntiles) stage_write(buf ^ 1, true, false);
       __syncthreads();
     }
   } else {  // MODE_PV: O = P V with P from HBM (materialise mode)
@@ -337,7 +287,10 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
 //    tile's max exceeds it by more than kRescaleThr (log2 units), so p stays <= 2^kRescaleThr;
 //    the decision precedes the tile's exponentiation (the safe order), wave-uniform;
 //  * no key-mask support (materialise mode only) and masking code only for a partial last tile.
-template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES>
+//  * EXACT (launches that keep maps): the row sum is the f32 sum of the exponentials (VALU adds),
+//    not the MFMA sum of their bf16 roundings, so the lse that self_maps_kernel normalises the
+//    stored maps with is f32-exact (a peaky row's bf16 rounding would otherwise be ~2e-3).
+template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, bool EXACT = false>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -356,7 +309,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
   constexpr int VBUF = BK * VS;
   constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
   constexpr int VBYTES = 2 * VBUF * (int)sizeof(EV);
-  constexpr bool kOnes = DV > D;                 // row sum through the PV MFMA
+  constexpr bool kOnes = DV > D && !EXACT;       // row sum through the PV MFMA
   constexpr int kLdt = D / 32;                   // O^T tile / register / lane-half holding row D
   constexpr int kLrr = D % 32;
   constexpr int kLh = (kLrr >> 2) & 1;
@@ -544,6 +497,89 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
       }
     // row log-sum-exp for the backward pass (log2 domain, scale folded: p = exp2(c s - lse))
     if (a.lse && hh == 0) a.lse[(int64_t)(n * a.H + h) * a.P + p] = m_run + __log2f(l);
+  }
+}
+
+// ====================================================================== stored self maps
+// AttentionStore epilogue of the self layers whose maps are kept (main.py:129-142, P <= 32^2;
+// the stored tensor is the post-injection map, main.py:181-195).  The fused kernel above has
+// produced O and every row's log-sum-exp (log2 domain, scale folded); this kernel recomputes
+// S = Q K^T in the NON-transposed orientation -- key on the lane, query on the accumulator
+// row -- so p = exp2(c s - lse) leaves as 128-byte row segments per half-wave: the read-add-
+// write of the running sum is the whole cost of the layer and is HBM-bound.  With the softmax
+// statistics known, keys split freely: one wave = 32 queries x kw keys, one workgroup = four
+// consecutive key chunks, so the grid is as wide as the map.  K fragments come straight from
+// global memory (a [K, d] head slice is L2-resident); no LDS, no barrier.
+template <typename IO, typename MQ, int D>
+__global__ __launch_bounds__(256) void self_maps_kernel(SelfArgs a, int kw, int n_kgroups) {
+  constexpr int DK = (D + 15) / 16 * 16;
+  constexpr int NKT = DK / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int li = lane & 31;
+
+  int rest = xcd_remap(blockIdx.x, gridDim.x);
+  const int kg = rest % n_kgroups;
+  rest /= n_kgroups;
+  const int qb = rest % a.n_qtiles;
+  rest /= a.n_qtiles;
+  const int h = rest % a.H;
+  const int n = a.map_entry[rest / a.H];
+  const int src = a.qk_src[n];
+  const int P = a.P;
+  const int K = a.K;
+  const int k0 = (kg * 4 + wave) * kw;
+  if (k0 >= K) return;  // wave-uniform: no barrier in this kernel
+  const int k1 = min(K, k0 + kw);
+  const int p0 = qb * 32;
+  const float c = a.scale_log2;
+
+  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
+  typename MQ::frag qf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int col = 16 * t + 8 * hh;
+    qf[t] = (p0 + li < P && col < D) ? MQ::load_q(qp + (int64_t)(p0 + li) * a.ldq + col) : MQ::zero();
+  }
+  // per accumulator register r: query row p0 + acc_row(r, hh), its lse and map row
+  const float* const lse = a.lse + (int64_t)(n * a.H + h) * P;
+  float* const mp = a.store + (int64_t)(a.store_slot[n] + h) * P * (int64_t)K;
+  float lr[16];
+  bool rok[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = p0 + acc_row(r, hh);
+    rok[r] = row < P;
+    lr[r] = rok[r] ? lse[row] : 0.f;
+  }
+  const bool acc_on = a.store_accumulate != 0;
+  for (int kb = k0; kb < k1; kb += 32) {
+    const int key = kb + li;
+    const bool kok = key < k1;
+    float old[16];
+    if (acc_on) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        old[r] = (kok && rok[r]) ? mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] : 0.f;
+    }
+    const IO* const krow = kp + (int64_t)min(key, K - 1) * a.ldk;
+    f32x16_t acc = {};
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const int col = 16 * t + 8 * hh;
+      const typename MQ::frag kf = col < D ? MQ::load_q(krow + col) : MQ::zero();
+      MQ::mma(acc, qf[t], kf);  // A = Q rows, B = K rows: S (query x key), key on the lane
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (kok && rok[r]) {
+        float v = fast_exp2(fmaf(acc[r], c, -lr[r]));
+        if (acc_on) v += old[r];
+        mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] = v;
+      }
+    }
   }
 }
 
@@ -897,7 +933,10 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+  if (a.n_maps > 0)  // the lse feeds stored maps: exact f32 row sums
+    hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
+  else
+    hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
@@ -927,7 +966,6 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);                                                              \
     dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);                                                        \
     switch (mode) {                                                                                          \
-      case MODE_STORE: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_STORE>), grid, block, 0, st, b); break; \
       case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break; \
       default: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;         \
     }                                                                                                        \
@@ -974,6 +1012,29 @@ static int dispatch_self(const SelfArgs& a, int d, int mode, hipStream_t st) {
   }
 }
 
+template <typename IO, typename MQ, int D>
+static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  // keys per wave: a quarter of the row (whole 32-key blocks), at most 256 -> a workgroup
+  // spans up to 1024 keys; wider rows take more key groups
+  const int kw = min(256, ((a.K + 3) / 4 + 31) / 32 * 32);
+  const int n_kgroups = (a.K + 4 * kw - 1) / (4 * kw);
+  b.n_qtiles = (a.P + 31) / 32;
+  dim3 grid(n_kgroups * b.n_qtiles * a.H * a.n_maps), block(256);
+  hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D>), grid, block, 0, st, b, kw, n_kgroups);
+  return hipGetLastError();
+}
+
+template <typename IO, typename MQ>
+static int dispatch_self_maps(const SelfArgs& a, int d, hipStream_t st) {
+  switch (d) {
+#define P2P_CASE(DD) case DD: return (int)launch_self_maps_d<IO, MQ, DD>(a, st);
+    P2P_FOR_EACH_D(P2P_CASE)
+#undef P2P_CASE
+    default: return P2P_E_HEAD_DIM;
+  }
+}
+
 template <typename IO, typename MQ, typename MP>
 static int dispatch_cross(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
@@ -993,6 +1054,16 @@ int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipS
   }
   if (io_dtype == P2P_DTYPE_F32) return dispatch_self<float, QkSplit, MmaBf16>(a, d, mode, st);
   return dispatch_self<uint16_t, QkBf16<uint16_t>, MmaBf16>(a, d, mode, st);
+}
+
+int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st) {
+  if (a.n_maps < 1) return 0;
+  if (compute == P2P_COMPUTE_F32) {
+    if (io_dtype != P2P_DTYPE_F32) return P2P_E_DTYPE;
+    return dispatch_self_maps<float, QkF32>(a, d, st);
+  }
+  if (io_dtype == P2P_DTYPE_F32) return dispatch_self_maps<float, QkSplit>(a, d, st);
+  return dispatch_self_maps<uint16_t, QkBf16<uint16_t>>(a, d, st);
 }
 
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st) {

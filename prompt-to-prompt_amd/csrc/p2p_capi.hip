@@ -31,6 +31,9 @@ int check_tensors(const p2p_attn_tensors* t, bool need_q, bool need_k, bool need
   return 0;
 }
 
+void no_maps(SelfArgs& a) { a.n_maps = 0; }
+void no_maps(CrossArgs&) {}
+
 template <typename A>
 void fill_common(A& a, const p2p_attn_tensors* t) {
   a.q = t->q; a.k = t->k; a.v = t->v; a.o = t->o;
@@ -41,6 +44,7 @@ void fill_common(A& a, const p2p_attn_tensors* t) {
   a.n_qtiles = 0;
   a.store = nullptr;
   a.store_accumulate = 0;
+  no_maps(a);
 }
 
 int self_variant() {
@@ -68,7 +72,7 @@ const char* p2p_error_string(int code) {
 }
 
 int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* store, const int32_t* store_slot,
-                      int32_t store_accumulate, p2p_stream_t stream) {
+                      int32_t store_accumulate, float* lse_workspace, p2p_stream_t stream) {
   int rc = check_tensors(t, true, true, true, true);
   if (rc) return rc;
   SelfArgs a;
@@ -77,18 +81,23 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
   a.lse = nullptr;
   a.probs = nullptr;
   a.key_mask = nullptr;
-  bool any_store = false;
   for (int n = 0; n < t->n_batch; ++n) {
     a.qk_src[n] = qk_src ? qk_src[n] : n;
     if (a.qk_src[n] < 0 || a.qk_src[n] >= t->n_batch) return P2P_E_BATCH;
     a.store_slot[n] = (store && store_slot) ? store_slot[n] : -1;
-    any_store |= a.store_slot[n] >= 0;
+    if (a.store_slot[n] >= 0) a.map_entry[a.n_maps++] = n;
   }
-  if (any_store && !aligned16(store)) return P2P_E_ALIGN;
-  a.store = any_store ? store : nullptr;
-  a.store_accumulate = store_accumulate ? 1 : 0;
-  return run_self(a, t->io_dtype, t->compute, t->head_dim, any_store ? MODE_STORE_ : MODE_FUSED_,
-                  (hipStream_t)stream);
+  if (a.n_maps > 0) {
+    if (!lse_workspace) return P2P_E_ARG;
+    if (!aligned16(store) || !aligned16(lse_workspace)) return P2P_E_ALIGN;
+    a.store = store;
+    a.store_accumulate = store_accumulate ? 1 : 0;
+    a.lse = lse_workspace;
+  }
+  // O (and, when maps are kept, every row's lse) in one fused pass; then the stored maps
+  rc = run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_FUSED_, (hipStream_t)stream);
+  if (rc || a.n_maps == 0) return rc;
+  return run_self_maps(a, t->io_dtype, t->compute, t->head_dim, (hipStream_t)stream);
 }
 
 int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32_t n_groups, float* store,

@@ -26,6 +26,8 @@ struct SelfArgs {
   float* lse;                  // optional [N*H, P] row log-sum-exp output (fused mode, autograd)
   int qk_src[P2P_MAX_BATCH];
   int store_slot[P2P_MAX_BATCH];
+  int n_maps;                  // self_maps_kernel: entries in map_entry
+  int map_entry[P2P_MAX_BATCH];  // self_maps_kernel: the stored entries (store_slot >= 0)
 };
 
 struct CrossArgs {
@@ -54,9 +56,12 @@ struct CrossArgs {
   int grp_flags[P2P_MAX_GROUPS];
 };
 
-enum { MODE_FUSED_ = 0, MODE_STORE_ = 1, MODE_PROBS_ = 2, MODE_PV_ = 3 };
+enum { MODE_FUSED_ = 0, MODE_PROBS_ = 2, MODE_PV_ = 3 };
 
 int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st);
+// AttentionStore epilogue of the self layers whose maps are kept: p = exp2(c s - lse) for the
+// entries a.map_entry[0 .. n_maps) (a.lse filled by a preceding MODE_FUSED launch)
+int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);

@@ -27,7 +27,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class HipError(RuntimeError):
@@ -90,7 +90,7 @@ def lib():
         L.p2p_abi_version.restype = ctypes.c_int
         L.p2p_error_string.restype = ctypes.c_char_p
         L.p2p_error_string.argtypes = [ctypes.c_int]
-        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp]
+        L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp, vp]
         L.p2p_cross_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, i32, vp, vp, i32, vp]
         L.p2p_attn_probs.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp]
         L.p2p_attn_pv.argtypes = [ctypes.POINTER(AttnTensors), vp, vp]
@@ -177,6 +177,19 @@ def _i32_array(vals: Sequence[int]):
     return arr
 
 
+_LSE_WS = {}
+
+
+def _lse_workspace(device, numel):
+    """Per-device f32 scratch for the row log-sum-exp of a self launch that keeps maps (grown,
+    never shrunk; stream-ordered reuse: every launch on the device's current stream)."""
+    buf = _LSE_WS.get(device)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
+        _LSE_WS[device] = buf
+    return buf
+
+
 def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None, store_slot=None,
               accumulate=False):
     t = make_tensors(q, k, v, o, heads, scale, compute)
@@ -185,11 +198,14 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
     if store is not None:
         _require_cuda(store)
         assert store.dtype == torch.float32 and store.is_contiguous()
+    ws = None
+    if store is not None and store_slot is not None and any(int(s) >= 0 for s in store_slot):
+        ws = _lse_workspace(q.device, t.n_batch * t.n_heads * t.n_query).data_ptr()
     obs = LAUNCH_OBSERVER
     if obs is not None:
         obs.before("self", t)
     rc = lib().p2p_self_attn_fwd(ctypes.byref(t), src, store.data_ptr() if store is not None else None,
-                                 slots, int(bool(accumulate)), _stream(q.device))
+                                 slots, int(bool(accumulate)), ws, _stream(q.device))
     if obs is not None:
         obs.after("self", t)
     _check(rc, "p2p_self_attn_fwd")

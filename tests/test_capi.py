@@ -63,14 +63,23 @@ def _tensors(**kw):
 def test_self_attn_rejects(kw, code):
     L = _hip.lib()
     t = _tensors(**kw)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None) == code
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, None, None, 0, None, None) == code
 
 
 def test_self_attn_rejects_bad_source_index():
     L = _hip.lib()
     t = _tensors()
     src = (ctypes.c_int32 * 8)(0, 1, 2, 3, 4, 5, 6, 99)
-    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None) == -5
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), src, None, None, 0, None, None) == -5
+
+
+def test_self_attn_store_needs_lse_workspace():
+    # a kept map needs the row log-sum-exp scratch (rejected before any launch)
+    L = _hip.lib()
+    t = _tensors(n_query=1024, n_key=1024, head_dim=80)
+    slots = (ctypes.c_int32 * 8)(-1, -1, -1, -1, 0, 8, 16, 24)
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, 64, slots, 1, None, None) == -1
+    assert L.p2p_self_attn_fwd(ctypes.byref(t), None, 64, slots, 1, 72, None) == -6
 
 
 def test_cross_attn_rejects():

@@ -1,7 +1,8 @@
 """AttentionStore epilogue cost of the self kernels (main.py:129-142 default: self maps kept for
 P <= 32^2): G2/G6 (P = K = 1024, d = 80) and G3 (P = K = 256, d = 160), cond half (4 entries x 8
 heads) accumulated into the running sum, vs the fused kernel without a store.  Achieved HBM GB/s
-counts the map read + write of the running sum (8 B per element) plus q/k/v/o."""
+counts the map read + write of the running sum (8 B per element) plus q/k/v/o.  store_us = the fused
+pass (O + row lse, all N entries) + self_maps_kernel (the kept maps, cond half)."""
 import json
 import os
 import statistics
