@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--unet-dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--compute", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--store-self", action="store_true",
+                    help="also keep the 32x32/16x16/8x8 SELF maps (main.py AttentionStore default); the\n                         north-star workload keeps only the maps AttentionStore/LocalBlend read")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,7 +146,8 @@ def main():
     _hip.LAUNCH_OBSERVER = timer
 
     def group(seed):
-        ctrl = pl.make_replace_controller(prompts, args.ddim_steps, device=dev)
+        ctrl = pl.make_replace_controller(prompts, args.ddim_steps, device=dev,
+                                          store_self_maps=args.store_self)
         return pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(seed), num_steps=args.ddim_steps)
 
     # groups (seeds) partitioned across ranks round-robin: no collective on the data path
@@ -181,7 +184,7 @@ def main():
                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "algorithmic_bytes": 4.0 * 8 * 4096 * 320 * 2,
-                    "kernel": "self_attn_kernel G1/G7 (P=K=4096, d=40, N=8, H=8)",
+                    "kernel": "self_attn_fused_kernel G1/G7 (P=K=4096, d=40, N=8, H=8)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
         cpu = None
@@ -196,7 +199,7 @@ def main():
             "data": "synthetic (random-init SD-v1.4-shaped U-Net, seeded x_T, stand-in text context)",
             "config": {"workload": "configs[1]: SD-v1.4 512x512 AttentionReplace + LocalBlend, 1 source + 3 edits, "
                                    f"{args.ddim_steps} DDIM, CFG 7.5", "global_batch": 8 * world,
-                       "unet_dtype": args.unet_dtype, "parallelism": f"replicas x{world} (groups by seed)"},
+                       "unet_dtype": args.unet_dtype, "self_maps_kept": args.store_self, "parallelism": f"replicas x{world} (groups by seed)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
