@@ -65,10 +65,13 @@ def test_self_attention_output(cuda, geom, compute):
 
 @pytest.mark.parametrize("compute,qscale,tol", [("f32", 1.0, 1e-5), ("f32", 12.0, 1e-5),
                                                ("bf16", 1.0, 2e-3), ("bf16", 8.0, 2e-3), ("bf16", 16.0, 2e-3)])
-@pytest.mark.parametrize("geom", [(2, 1024, 1024, 2, 80), (2, 256, 256, 4, 160), (2, 64, 4096, 2, 40)],
+@pytest.mark.parametrize("geom", [(2, 1024, 1024, 2, 80), (2, 256, 256, 4, 160), (2, 64, 4096, 2, 40),
+                                  (2, 40, 1100, 2, 64), (3, 16, 16, 2, 32)],
                          ids=lambda g: "x".join(map(str, g)))
 def test_self_attention_store_probs(cuda, geom, compute, qscale, tol):
-    """The AttentionStore epilogue writes exact probabilities (two-pass mode)."""
+    """The AttentionStore epilogue writes exact probabilities (fused pass's lse + self_maps_kernel);
+    ragged cases: a partial query tile (P = 40, 16), a partial last key block and two key groups
+    (K = 1100 > 4 x 256), d without a padding column (64, 32)."""
     N, P, K, H, d = geom
     q, k, v = make_qkv(N, P, K, H, d, torch.float32, qscale=qscale, seed=3)
     o = torch.empty_like(q)
