@@ -5,7 +5,7 @@
 //                     (main.py:169-174 / null_text.py:224-230) as a batch index remap.
 // self_maps_kernel  : the AttentionStore epilogue (main.py:129-142) for self layers whose maps
 //                     are kept, from the fused kernel's row log-sum-exp.
-// self_attn_kernel  : the materialise protocol (probabilities to HBM, then P V).
+// self_probs_kernel / self_pv_kernel : the materialise protocol (probabilities to HBM, then P V).
 // cross_attn_kernel : cross-attention over the 77 text tokens with the P2P cross edit
 //                     (AttentionControlEdit.forward, main.py:180-197) applied in registers
 //                     between the exact softmax and PV, for every prompt group.
@@ -36,35 +36,27 @@ template <>
 __device__ __forceinline__ uint16_t one_elem<uint16_t>() { return 0x3F80; }  // bf16 1.0
 
 // ====================================================================== self attention
-// The materialise protocol's two kernels (the fused path is self_attn_fused_kernel below):
-// MODE_PROBS : pass 1 row max/sum, pass 2 exact P written to HBM
-// MODE_PV    : O = P V with P read from HBM
-enum { MODE_FUSED = 0, MODE_PROBS = 2, MODE_PV = 3 };
+enum { MODE_FUSED = 0, MODE_PV = 3 };
 
-template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, int MODE>
-__global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
-  using EK = typename MQ::elem;
+// The materialise protocol's second half (ptp_utils.py:206-207 after a controller rewrote attn):
+// O[n] = probs[n*H + h] V[n] with the probabilities read from HBM.  Same Oᵀ = Vᵀ Pᵀ form as the
+// fused kernel: the lane (query) reads its row's keys in the Sᵀ accumulator order, 4 consecutive
+// keys per 16-byte load (keys (r&3) + 8(r>>2) + 4h), so a half-wave covers 32 bytes of each of its
+// 32 rows per instruction and four instructions a 128-byte segment; V tiles are staged in LDS.
+template <typename IO, typename MP, int D, int BK, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void self_pv_kernel(SelfArgs a) {
   using EV = typename MP::elem;
-  constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
-  constexpr int NKT = DK / 16;
   constexpr int NDT = DV / 32;
   constexpr int NSB = BK / 32;
-  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
   constexpr int VS = (MP::kElemBytes == 2) ? VStrideBf16<DV>::value : DV;
   constexpr int NT = 64 * WAVES;
   constexpr int CPR = D / 8;
   constexpr int NCH = (BK * CPR + NT - 1) / NT;
-  constexpr bool kNeedK = MODE != MODE_PV;
-  constexpr bool kNeedV = MODE == MODE_PV;
-  constexpr int KPLANE = BK * KS;                       // elements per K plane
-  constexpr int KBUF = kNeedK ? KPLANE * MQ::planes : 0;  // elements per K buffer
-  constexpr int VBUF = kNeedV ? BK * VS : 0;
-  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
+  constexpr int VBUF = BK * VS;
   constexpr int VBYTES = 2 * VBUF * (int)sizeof(EV);
-  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
-  EK* const Ks = reinterpret_cast<EK*>(smem);
-  EV* const Vs = reinterpret_cast<EV*>(smem + KBYTES);
+  __shared__ __attribute__((aligned(16))) char smem[VBYTES + 16];
+  EV* const Vs = reinterpret_cast<EV*>(smem);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -77,84 +69,37 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
   const int nh = logical / a.n_qtiles;
   const int h = nh % a.H;
   const int n = nh / a.H;
-  const int src = a.qk_src[n];
   const int p = qt * 32 * WAVES + wave * 32 + qi;
   const bool prow = p < a.P;
   const int K = a.K;
-  const float c = a.scale_log2;
-
-  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
-  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
   const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
   IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
+  const float* const pp = a.probs + ((int64_t)(n * a.H + h) * a.P + (prow ? p : 0)) * (int64_t)K;
+  const bool vec4 = (K & 3) == 0;
 
-  // zero the LDS image once: pad columns [D, DK) / [D, DV) and rows >= K stay zero.
-  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
+  // zero the LDS image once: pad columns [D, DV) and rows >= K stay zero
+  for (int i = tid; i < VBYTES / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
 
-  // Q fragments stay in registers for the whole key loop.
-  typename MQ::frag qf[NKT];
-  if constexpr (kNeedK) {
-#pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      const int col = 16 * t + 8 * hh;
-      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
-    }
-  }
-
-  Chunk8<IO> kreg[NCH], vreg[NCH];
-  auto stage_load = [&](int kt, bool withK, bool withV) {
+  Chunk8<IO> vreg[NCH];
+  auto stage_load = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
       const int key = kt * BK + row;
-      const bool ok = cidx < BK * CPR && key < K;
-      if (withK) {
-        if (ok) kreg[i].load(kp + (int64_t)key * a.ldk + ch * 8); else kreg[i].clear();
-      }
-      if (withV) {
-        if (ok) vreg[i].load(vp + (int64_t)key * a.ldv + ch * 8); else vreg[i].clear();
-      }
+      if (cidx < BK * CPR && key < K) vreg[i].load(vp + (int64_t)key * a.ldv + ch * 8); else vreg[i].clear();
     }
   };
-  auto stage_write = [&](int buf, bool withK, bool withV) {
+  auto stage_write = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       if (cidx < BK * CPR) {
         const int row = cidx / CPR;
         const int ch = cidx - row * CPR;
-        if (withK) MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
-        if (withV) vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
+        vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
       }
-    }
-  };
-
-  // S^T block sb of the tile in buffer buf, masked beyond K (and by the optional key mask).
-  auto scores = [&](int buf, int kt, float (&sv)[NSB][16]) {
-    const EK* Kb = Ks + buf * KBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      f32x16_t acc = {};
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
-        MQ::mma(acc, fa, qf[t]);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
-    }
-    if ((kt + 1) * BK > K || a.key_mask) {
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * BK + sb * 32 + acc_row(r, hh);
-          if (key >= K) sv[sb][r] = -INFINITY;
-          else if (a.key_mask && !a.key_mask[(int64_t)((n * a.H + h) % a.N) * K + key])
-            sv[sb][r] = -3.402823466e38f;
-        }
     }
   };
 
@@ -162,124 +107,51 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_kernel(SelfArgs a) {
   f32x16_t O[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
-
-  float m_run = -INFINITY, l_run = 0.f;
-
-  if constexpr (MODE == MODE_PROBS) {
-    // ---- pass 1: exact row max and row sum
-    __syncthreads();
-    stage_load(0, true, false);
-    stage_write(0, true, false);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < ntiles) stage_load(kt + 1, true, false);
-      float sv[NSB][16];
-      scores(buf, kt, sv);
-      float mx = -INFINITY;
+  __syncthreads();
+  stage_load(0);
+  stage_write(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_load(kt + 1);
+    float sv[NSB][16];
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
+    for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mnew = fmaxf(m_run, mx * c);
-      float ls = 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const int key = kt * BK + sb * 32 + 8 * g + 4 * hh;
+        if (vec4 && prow && key < K) {  // K % 4 == 0: the 4 keys are all in range together
+          const f32x4_t x = *reinterpret_cast<const f32x4_t*>(pp + key);
+          sv[sb][4 * g] = x[0];
+          sv[sb][4 * g + 1] = x[1];
+          sv[sb][4 * g + 2] = x[2];
+          sv[sb][4 * g + 3] = x[3];
+        } else {
 #pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ls += fast_exp2(fmaf(sv[sb][r], c, -mnew));
-      l_run = fmaf(l_run, fast_exp2(m_run - mnew), ls);
-      m_run = mnew;
-      if (kt + 1 < ntiles) stage_write(buf ^ 1, true, false);
-      __syncthreads();
-    }
-    const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
-    // ---- pass 2: exact probabilities -> HBM
-    const int slot = a.store_slot[n];
-    float* const mp = (a.store && slot >= 0 && prow)
-                          ? a.store + ((int64_t)(slot + h) * a.P + p) * (int64_t)K
-                          : nullptr;
-    const bool vec4 = (K & 3) == 0;
-    stage_load(0, true, false);
-    stage_write(0, true, false);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < ntiles) stage_load(kt + 1, true, false);
-      float sv[NSB][16];
-      scores(buf, kt, sv);
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sv[sb][r] = fast_exp2(fmaf(sv[sb][r], c, -m_run)) * inv;
-      if (mp) {
-#pragma unroll
-        for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int key = kt * BK + sb * 32 + 8 * g + 4 * hh;
-            if (vec4) {
-              if (key < K) {
-                f32x4_t v = {sv[sb][4 * g], sv[sb][4 * g + 1], sv[sb][4 * g + 2], sv[sb][4 * g + 3]};
-                f32x4_t* dst = reinterpret_cast<f32x4_t*>(mp + key);
-                if (a.store_accumulate) v += *dst;
-                *dst = v;
-              }
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (key + e < K) {
-                  const float v = sv[sb][4 * g + e];
-                  mp[key + e] = a.store_accumulate ? mp[key + e] + v : v;
-                }
-            }
-          }
+          for (int e = 0; e < 4; ++e) sv[sb][4 * g + e] = (prow && key + e < K) ? pp[key + e] : 0.f;
+        }
       }
-      if (kt + 1 < ntiles) stage_write(buf ^ 1, true, false);
-      __syncthreads();
-    }
-  } else {  // MODE_PV: O = P V with P from HBM (materialise mode)
-    const float* const pp = a.probs + ((int64_t)(n * a.H + h) * a.P + (prow ? p : 0)) * (int64_t)K;
+    const EV* Vb = Vs + buf * VBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
+    if (kt + 1 < ntiles) stage_write(buf ^ 1);
     __syncthreads();
-    stage_load(0, false, true);
-    stage_write(0, false, true);
-    __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < ntiles) stage_load(kt + 1, false, true);
-      float sv[NSB][16];
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * BK + sb * 32 + acc_row(r, hh);
-          sv[sb][r] = (prow && key < K) ? pp[key] : 0.f;
-        }
-      const EV* Vb = Vs + buf * VBUF;
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
-      if (kt + 1 < ntiles) stage_write(buf ^ 1, false, true);
-      __syncthreads();
-    }
   }
-
-  if constexpr (MODE != MODE_PROBS) {
-    if (prow) {
+  if (prow) {
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int dd = dt * 32 + 8 * g + 4 * hh;
-          if (dd < D)
-            store4(op + (int64_t)p * a.ldo + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2],
-                   O[dt][4 * g + 3]);
-        }
-    }
+      for (int g = 0; g < 4; ++g) {
+        const int dd = dt * 32 + 8 * g + 4 * hh;
+        if (dd < D)
+          store4(op + (int64_t)p * a.ldo + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2],
+                 O[dt][4 * g + 3]);
+      }
   }
 }
 
 // ====================================================================== fused self attention
-// The hot kernel (G1/G7: P = K = 4096, d = 40).  Differences from self_attn_kernel's FUSED mode:
+// The hot kernel (G1/G7: P = K = 4096, d = 40).  Beyond a plain online-softmax (flash) loop:
 //  * row sums come out of the PV MFMA: V's first padding column (d..DV) is set to 1 in LDS, so
 //    O^T row d accumulates sum_k bf16(p_k) -- the same weights the PV uses -- with no VALU adds
 //    (only when DV > D; otherwise the sum is a per-lane VALU sum as before);
@@ -578,6 +450,132 @@ __global__ __launch_bounds__(256) void self_maps_kernel(SelfArgs a, int kw, int 
         float v = fast_exp2(fmaf(acc[r], c, -lr[r]));
         if (acc_on) v += old[r];
         mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] = v;
+      }
+    }
+  }
+}
+
+// ====================================================================== materialised probabilities
+// The materialise protocol's first half (controllers that override forward(attn, ...),
+// main.py:85-98): probs[n*H + h] = softmax(Q K^T * scale), f32 [N*H, P, K] (ptp_utils.py:195-204,
+// with the optional key mask of :197-201 and its head-major repeat of the mask rows).  HBM-bound
+// (G1: 4.3 GB written per layer), so the store side follows self_maps_kernel: one workgroup = 32
+// queries x all keys, the four waves split the keys.  Pass 1 (S^T, query on the lane: reductions
+// stay in the lane) gives each wave's partial row max / sum, combined across the waves in LDS;
+// pass 2 recomputes S with the key on the lane and writes p = exp2(t - M) / L as 128-byte row
+// segments per half-wave.  A masked key scores -FLT_MAX after the scale (the reference fills the
+// scaled logits with -finfo.max): p = 0 beside any unmasked key, 1/K on a fully masked row.
+template <typename IO, typename MQ, int D>
+__global__ __launch_bounds__(256) void self_probs_kernel(SelfArgs a, int kw) {
+  constexpr int DK = (D + 15) / 16 * 16;
+  constexpr int NKT = DK / 16;
+  constexpr float kNeg = -3.402823466e38f;
+  __shared__ float sm[4][32], sl[4][32];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int li = lane & 31;
+
+  int rest = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = rest % a.n_qtiles;
+  rest /= a.n_qtiles;
+  const int h = rest % a.H;
+  const int n = rest / a.H;
+  const int P = a.P;
+  const int K = a.K;
+  const int k0 = wave * kw;
+  const int k1 = min(K, k0 + kw);  // empty for trailing waves when K < 4 kw: they still sync
+  const int p0 = qb * 32;
+  const float c = a.scale_log2;
+  const uint8_t* const km = a.key_mask ? a.key_mask + (int64_t)((n * a.H + h) % a.N) * K : nullptr;
+
+  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)n * a.bsq + h * D;
+  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)n * a.bsk + h * D;
+  typename MQ::frag qf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int col = 16 * t + 8 * hh;
+    qf[t] = (p0 + li < P && col < D) ? MQ::load_q(qp + (int64_t)(p0 + li) * a.ldq + col) : MQ::zero();
+  }
+  auto scores = [&](int kb, bool transposed, f32x16_t& acc) {
+    const IO* const krow = kp + (int64_t)min(kb + li, K - 1) * a.ldk;
+    acc = f32x16_t{};
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const int col = 16 * t + 8 * hh;
+      const typename MQ::frag kf = col < D ? MQ::load_q(krow + col) : MQ::zero();
+      if (transposed) MQ::mma(acc, kf, qf[t]);  // S^T: key on the accumulator row, query on the lane
+      else MQ::mma(acc, qf[t], kf);             // S:   query on the accumulator row, key on the lane
+    }
+  };
+
+  // ---- pass 1: this wave's row max / sum over its keys (t = s * c, or kNeg when masked)
+  float m = -INFINITY, l = 0.f;
+#pragma unroll 4
+  for (int kb = k0; kb < k1; kb += 32) {
+    f32x16_t acc;
+    scores(kb, true, acc);
+    float tv[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb + acc_row(r, hh);
+      tv[r] = key >= k1 ? -INFINITY : (km && !km[key]) ? kNeg : acc[r] * c;
+      mx = fmaxf(mx, tv[r]);
+    }
+    const float mnew = fmaxf(m, mx);
+    if (mnew != -INFINITY) {
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ls += fast_exp2(tv[r] - mnew);
+      l = fmaf(l, fast_exp2(m - mnew), ls);
+      m = mnew;
+    }
+  }
+  {  // the other half-wave holds the other keys of the same query
+    const float m2 = __shfl_xor(m, 32), l2 = __shfl_xor(l, 32);
+    const float M = fmaxf(m, m2);
+    if (M != -INFINITY) {
+      l = (m == -INFINITY ? 0.f : l * fast_exp2(m - M)) + (m2 == -INFINITY ? 0.f : l2 * fast_exp2(m2 - M));
+      m = M;
+    }
+  }
+  if (hh == 0) {
+    sm[wave][li] = m;
+    sl[wave][li] = l;
+  }
+  __syncthreads();
+  // per accumulator register r of the S orientation: query row p0 + acc_row(r, hh)
+  float Mr[16], Ir[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = acc_row(r, hh);
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w][row]);
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) L += sm[w][row] == -INFINITY ? 0.f : sl[w][row] * fast_exp2(sm[w][row] - M);
+    Mr[r] = M;
+    Ir[r] = 1.f / L;
+  }
+
+  // ---- pass 2: exact probabilities, key on the lane
+  float* const pp = a.store + (int64_t)(n * a.H + h) * P * (int64_t)K;
+#pragma unroll 2
+  for (int kb = k0; kb < k1; kb += 32) {
+    f32x16_t acc;
+    scores(kb, false, acc);
+    const int key = kb + li;
+    if (key < k1) {
+      const bool masked = km && !km[key];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = p0 + acc_row(r, hh);
+        if (row < P) {
+          const float x = masked ? kNeg - Mr[r] : fmaf(acc[r], c, -Mr[r]);
+          pp[(int64_t)row * K + key] = fast_exp2(x) * Ir[r];
+        }
       }
     }
   }
@@ -960,18 +958,12 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     else launch_fused<IO, MQ, MP, D, BK, 4>(a, st);
     return hipGetLastError();
   }
+  // MODE_PV: the materialise protocol's P V
   SelfArgs b = a;
-#define P2P_LAUNCH_SELF(W)                                                                                   \
-  {                                                                                                          \
-    b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);                                                              \
-    dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);                                                        \
-    switch (mode) {                                                                                          \
-      case MODE_PROBS: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PROBS>), grid, block, 0, st, b); break; \
-      default: hipLaunchKernelGGL((self_attn_kernel<IO, MQ, MP, D, BK, W, MODE_PV>), grid, block, 0, st, b); break;         \
-    }                                                                                                        \
-  }
-  if (a.P <= 64) P2P_LAUNCH_SELF(2) else P2P_LAUNCH_SELF(4)
-#undef P2P_LAUNCH_SELF
+  constexpr int W = 4;
+  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_pv_kernel<IO, MP, D, BK, W>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -1025,6 +1017,26 @@ static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <typename IO, typename MQ, int D>
+static hipError_t launch_self_probs_d(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  const int kw = ((a.K + 3) / 4 + 31) / 32 * 32;  // keys per wave: a quarter of the row
+  b.n_qtiles = (a.P + 31) / 32;
+  dim3 grid(b.n_qtiles * a.H * a.N), block(256);
+  hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D>), grid, block, 0, st, b, kw);
+  return hipGetLastError();
+}
+
+template <typename IO, typename MQ>
+static int dispatch_self_probs(const SelfArgs& a, int d, hipStream_t st) {
+  switch (d) {
+#define P2P_CASE(DD) case DD: return (int)launch_self_probs_d<IO, MQ, DD>(a, st);
+    P2P_FOR_EACH_D(P2P_CASE)
+#undef P2P_CASE
+    default: return P2P_E_HEAD_DIM;
+  }
+}
+
 template <typename IO, typename MQ>
 static int dispatch_self_maps(const SelfArgs& a, int d, hipStream_t st) {
   switch (d) {
@@ -1054,6 +1066,15 @@ int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipS
   }
   if (io_dtype == P2P_DTYPE_F32) return dispatch_self<float, QkSplit, MmaBf16>(a, d, mode, st);
   return dispatch_self<uint16_t, QkBf16<uint16_t>, MmaBf16>(a, d, mode, st);
+}
+
+int run_self_probs(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st) {
+  if (compute == P2P_COMPUTE_F32) {
+    if (io_dtype != P2P_DTYPE_F32) return P2P_E_DTYPE;
+    return dispatch_self_probs<float, QkF32>(a, d, st);
+  }
+  if (io_dtype == P2P_DTYPE_F32) return dispatch_self_probs<float, QkSplit>(a, d, st);
+  return dispatch_self_probs<uint16_t, QkBf16<uint16_t>>(a, d, st);
 }
 
 int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st) {

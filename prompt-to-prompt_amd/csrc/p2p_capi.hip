@@ -159,7 +159,7 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
     a.qk_src[n] = n;
     a.store_slot[n] = n * t->n_heads;
   }
-  return run_self(a, t->io_dtype, t->compute, t->head_dim, MODE_PROBS_, (hipStream_t)stream);
+  return run_self_probs(a, t->io_dtype, t->compute, t->head_dim, (hipStream_t)stream);
 }
 
 int p2p_attn_pv(const p2p_attn_tensors* t, const float* probs, p2p_stream_t stream) {

@@ -56,12 +56,14 @@ struct CrossArgs {
   int grp_flags[P2P_MAX_GROUPS];
 };
 
-enum { MODE_FUSED_ = 0, MODE_PROBS_ = 2, MODE_PV_ = 3 };
+enum { MODE_FUSED_ = 0, MODE_PV_ = 3 };
 
 int run_self(const SelfArgs& a, int io_dtype, int compute, int d, int mode, hipStream_t st);
 // AttentionStore epilogue of the self layers whose maps are kept: p = exp2(c s - lse) for the
 // entries a.map_entry[0 .. n_maps) (a.lse filled by a preceding MODE_FUSED launch)
 int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st);
+// materialise protocol: probs (a.store) [N*H, P, K] = softmax(Q K^T * scale), optional key mask
+int run_self_probs(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);

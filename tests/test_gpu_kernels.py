@@ -128,7 +128,8 @@ def test_self_attention_bf16_io(cuda, io):
 
 
 @pytest.mark.parametrize("compute,tol", [("f32", 1e-5), ("bf16", 2e-3)])
-@pytest.mark.parametrize("geom", [(4, 4096, 77, 8, 40), (4, 256, 77, 8, 160), (6, 100, 77, 2, 16)],
+@pytest.mark.parametrize("geom", [(4, 4096, 77, 8, 40), (4, 256, 77, 8, 160), (6, 100, 77, 2, 16),
+                                  (2, 1024, 1024, 2, 80), (2, 40, 1100, 2, 64), (2, 33, 130, 2, 8)],
                          ids=lambda g: "x".join(map(str, g)))
 def test_probs_and_pv_materialise(cuda, geom, compute, tol):
     N, P, K, H, d = geom
@@ -202,12 +203,15 @@ def test_cross_edit_paths(cuda, weight, compute, tol, geom):
     assert (o - ref_out(want, v, H)).abs().max().item() < o_tol(v, compute)
 
 
-def test_key_mask_materialise(cuda):
-    N, P, K, H, d = 2, 64, 77, 2, 16
+@pytest.mark.parametrize("K", [77, 1100])
+def test_key_mask_materialise(cuda, K):
+    """Partial masks zero the masked keys; a fully masked row is uniform (softmax of -finfo.max)."""
+    N, P, H, d = 3, 64, 2, 16
     q, k, v = make_qkv(N, P, K, H, d, torch.float32, seed=17)
     mask = torch.ones(N, K, dtype=torch.bool, device=cuda)
     mask[0, 50:] = False
     mask[1, :10] = False
+    mask[2, :] = False
     probs = torch.empty(N * H, P, K, device=cuda)
     _hip.attn_probs(q, k, H, d ** -0.5, probs, compute="f32", key_mask=mask.to(torch.uint8))
     # ptp_utils.py:197-201: rows (n*H + h) take mask row (n*H + h) % N (head-major repeat)
