@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--unet-dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--compute", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--groups-per-call", type=int, default=1,
+                    help="edit groups denoised per U-Net call (controllers.GroupBatch; a step = one such\n                         batch); 1 = configs[1] as quoted")
     ap.add_argument("--store-self", action="store_true",
                     help="also keep the 32x32/16x16/8x8 SELF maps (main.py AttentionStore default); the\n                         north-star workload keeps only the maps AttentionStore/LocalBlend read")
     args = ap.parse_args()
@@ -145,25 +147,37 @@ def main():
     timer = DominantKernelTimer()
     _hip.LAUNCH_OBSERVER = timer
 
-    def group(seed):
-        ctrl = pl.make_replace_controller(prompts, args.ddim_steps, device=dev,
-                                          store_self_maps=args.store_self)
-        return pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(seed), num_steps=args.ddim_steps)
+    G = args.groups_per_call
+
+    def make_ctrl():
+        return pl.make_replace_controller(prompts, args.ddim_steps, device=dev, store_self_maps=args.store_self)
+
+    def batch(seeds):
+        # one step: G edit groups (each 1 source + 3 edits, its own seed), one U-Net call per DDIM step
+        if G == 1:
+            return pl.run_edit_group(model, prompts, make_ctrl(), pl.seed_latent(seeds[0]),
+                                     num_steps=args.ddim_steps)[None]
+        from p2p_amd import controllers
+        ctrl = controllers.GroupBatch([make_ctrl() for _ in seeds])
+        lat = pl.run_edit_groups(model, [prompts] * G, ctrl, [pl.seed_latent(s) for s in seeds],
+                                 num_steps=args.ddim_steps)
+        return lat.reshape(G, len(prompts), *lat.shape[1:])
 
     # groups (seeds) partitioned across ranks round-robin: no collective on the data path
     from p2p_amd import sweep
-    all_seeds = list(range(world * (args.warmup + args.steps)))
+    all_seeds = list(range(world * (args.warmup + args.steps) * G))
     mine = sweep.partition(all_seeds, rank, world)
-    for s in mine[:args.warmup]:
-        group(s)
+    batches = [mine[i * G:(i + 1) * G] for i in range(args.warmup + args.steps)]
+    for b in batches[:args.warmup]:
+        batch(b)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timer.enabled = True
     t0 = time.perf_counter()
-    finals = torch.stack([group(s) for s in mine[args.warmup:]]).float()   # [steps, 4, 4, 64, 64]
+    finals = torch.cat([batch(b) for b in batches[args.warmup:]]).float()   # [steps * G, 4, 4, 64, 64]
     # one RCCL all-gather of the final latents at the end (the only inter-GPU traffic)
-    gathered = sweep.gather_latents(finals, world * args.steps, world)
+    gathered = sweep.gather_latents(finals, world * args.steps * G, world)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -173,24 +187,24 @@ def main():
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
-    assert gathered.shape[0] == world * args.steps and torch.isfinite(gathered).all()
+    assert gathered.shape[0] == world * args.steps * G and torch.isfinite(gathered).all()
 
     avg_ms, flops, n_launch = timer.summary()
     if rank == 0:
         peak = MFMA_PEAK_BF16_TFLOPS if args.compute == "bf16" else MFMA_PEAK_F32_TFLOPS
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms else None
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic() if G == 1 else (None, "no PMC pass at N = 8G")
         roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                    "algorithmic_bytes": 4.0 * 8 * 4096 * 320 * 2,
-                    "kernel": "self_attn_fused_kernel G1/G7 (P=K=4096, d=40, N=8, H=8)",
+                    "algorithmic_bytes": 4.0 * 8 * G * 4096 * 320 * 2,
+                    "kernel": f"self_attn_fused_kernel G1/G7 (P=K=4096, d=40, N={8 * G}, H=8)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.ddim_steps)
-        total = world * args.steps
+        total = world * args.steps * G
         line = {
             "metric": "edit-groups/sec (src+3 edits, SD1.4 512², 50 DDIM)",
             "value": total / elapsed, "unit": "edit-groups/s", "n_gpus": world, "steps": args.steps,
@@ -198,7 +212,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": args.compute,
             "data": "synthetic (random-init SD-v1.4-shaped U-Net, seeded x_T, stand-in text context)",
             "config": {"workload": "configs[1]: SD-v1.4 512x512 AttentionReplace + LocalBlend, 1 source + 3 edits, "
-                                   f"{args.ddim_steps} DDIM, CFG 7.5", "global_batch": 8 * world,
+                                   f"{args.ddim_steps} DDIM, CFG 7.5", "global_batch": 8 * G * world, "groups_per_call": G,
                        "unet_dtype": args.unet_dtype, "self_maps_kept": args.store_self, "parallelism": f"replicas x{world} (groups by seed)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
