@@ -182,7 +182,11 @@ _LSE_WS = {}
 
 def _lse_workspace(device, numel):
     """Per-device f32 scratch for the row log-sum-exp of a self launch that keeps maps (grown,
-    never shrunk; stream-ordered reuse: every launch on the device's current stream)."""
+    never shrunk; stream-ordered reuse: every launch on the device's current stream).  Under
+    hipGraph capture a call-local buffer from the graph's private pool is used instead, so a
+    replay never shares the scratch with eager launches."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(numel, dtype=torch.float32, device=device)
     buf = _LSE_WS.get(device)
     if buf is None or buf.numel() < numel:
         buf = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
