@@ -119,7 +119,8 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
  * protocol, main.py:85-98): probs[n*H + h] = softmax(Q K^T * scale) as an f32
  * [n_batch * n_heads, n_query, n_key] tensor (ptp_utils.py:195-204).  key_mask (nullable,
  * uint8 [n_batch, n_key], nonzero = keep) reproduces ptp_utils.py:197-201, including its
- * head-major repeat of the mask rows. */
+ * head-major repeat of the mask rows: a masked key scores -FLT_MAX after the scale, so it gets
+ * p = 0 beside any kept key and a fully masked row is uniform, 1/n_key. */
 int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* probs,
                    p2p_stream_t stream);
 
