@@ -203,6 +203,24 @@ def test_cross_edit_paths(cuda, weight, compute, tol, geom):
     assert (o - ref_out(want, v, H)).abs().max().item() < o_tol(v, compute)
 
 
+@pytest.mark.parametrize("geom", [(2, 1024, 1024, 2, 80), (2, 256, 4096, 2, 40), (3, 64, 77, 4, 160)],
+                         ids=lambda g: "x".join(map(str, g)))
+def test_probs_and_pv_materialise_bf16_inputs(cuda, geom):
+    """bf16 q/k/v (the production U-Net): one bf16 MFMA per k-step, exact products; probabilities
+    within 2e-3 of an fp32 softmax of the same bf16 data even on peaky rows, rows summing to 1."""
+    N, P, K, H, d = geom
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=8.0, seed=23)
+    probs = torch.empty(N * H, P, K, device=cuda)
+    _hip.attn_probs(q, k, H, d ** -0.5, probs)
+    p = ref_probs(q, k, H, d ** -0.5).reshape(N * H, P, K)
+    assert (probs - p).abs().max().item() < 2e-3
+    assert (probs.sum(-1) - 1).abs().max().item() < 1e-4
+    o = torch.empty_like(q)
+    _hip.attn_pv(probs, v, o, H)
+    want = ref_out(probs.reshape(N, H, P, K), v, H)
+    assert (o.float() - want).abs().max().item() < 2 * o_tol(v, "bf16")
+
+
 @pytest.mark.parametrize("K", [77, 1100])
 def test_key_mask_materialise(cuda, K):
     """Partial masks zero the masked keys; a fully masked row is uniform (softmax of -finfo.max)."""
