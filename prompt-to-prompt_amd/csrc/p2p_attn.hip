@@ -382,7 +382,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 // statistics known, keys split freely: one wave = 32 queries x kw keys, one workgroup = four
 // consecutive key chunks, so the grid is as wide as the map.  K fragments come straight from
 // global memory (a [K, d] head slice is L2-resident); no LDS, no barrier.
-template <typename IO, typename MQ, int D>
+template <typename IO, typename MQ, int D, int NB, bool NT>
 __global__ __launch_bounds__(256) void self_maps_kernel(SelfArgs a, int kw, int n_kgroups) {
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int NKT = DK / 16;
@@ -427,29 +427,45 @@ __global__ __launch_bounds__(256) void self_maps_kernel(SelfArgs a, int kw, int 
     lr[r] = rok[r] ? lse[row] : 0.f;
   }
   const bool acc_on = a.store_accumulate != 0;
-  for (int kb = k0; kb < k1; kb += 32) {
-    const int key = kb + li;
-    const bool kok = key < k1;
-    float old[16];
+  // NB key blocks per step: all their running-sum reads are issued before the first write (the
+  // compiler cannot hoist a later block's loads over stores to the same map)
+  for (int kb = k0; kb < k1; kb += 32 * NB) {
+    float old[NB][16];
     if (acc_on) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        old[r] = (kok && rok[r]) ? mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] : 0.f;
-    }
-    const IO* const krow = kp + (int64_t)min(key, K - 1) * a.ldk;
-    f32x16_t acc = {};
+      for (int j = 0; j < NB; ++j) {
+        const int key = kb + 32 * j + li;
 #pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      const int col = 16 * t + 8 * hh;
-      const typename MQ::frag kf = col < D ? MQ::load_q(krow + col) : MQ::zero();
-      MQ::mma(acc, qf[t], kf);  // A = Q rows, B = K rows: S (query x key), key on the lane
+        for (int r = 0; r < 16; ++r)
+          old[j][r] = (key < k1 && rok[r])
+                          ? (NT ? __builtin_nontemporal_load(mp + (int64_t)(p0 + acc_row(r, hh)) * K + key)
+                                : mp[(int64_t)(p0 + acc_row(r, hh)) * K + key])
+                          : 0.f;
+      }
+    }
+    f32x16_t acc[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const IO* const krow = kp + (int64_t)min(kb + 32 * j + li, K - 1) * a.ldk;
+      acc[j] = f32x16_t{};
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const int col = 16 * t + 8 * hh;
+        const typename MQ::frag kf = col < D ? MQ::load_q(krow + col) : MQ::zero();
+        MQ::mma(acc[j], qf[t], kf);  // A = Q rows, B = K rows: S (query x key), key on the lane
+      }
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (kok && rok[r]) {
-        float v = fast_exp2(fmaf(acc[r], c, -lr[r]));
-        if (acc_on) v += old[r];
-        mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] = v;
+    for (int j = 0; j < NB; ++j) {
+      const int key = kb + 32 * j + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (key < k1 && rok[r]) {
+          float v = fast_exp2(fmaf(acc[j][r], c, -lr[r]));
+          if (acc_on) v += old[j][r];
+          if constexpr (NT) __builtin_nontemporal_store(v, mp + (int64_t)(p0 + acc_row(r, hh)) * K + key);
+          else mp[(int64_t)(p0 + acc_row(r, hh)) * K + key] = v;
+        }
       }
     }
   }
@@ -1013,7 +1029,13 @@ static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
   const int n_kgroups = (a.K + 4 * kw - 1) / (4 * kw);
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(n_kgroups * b.n_qtiles * a.H * a.n_maps), block(256);
-  hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D>), grid, block, 0, st, b, kw, n_kgroups);
+  // non-temporal running-sum accesses (the map streams through once per step: -7.5 % at G2 with
+  // the maps HBM-resident; two key blocks per step measured +2 %, not instantiated).
+  // P2P_SELF_VARIANT=6 keeps plain accesses for A/B timing.
+  if (a.variant == 6)
+    hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, false>), grid, block, 0, st, b, kw, n_kgroups);
+  else
+    hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
   return hipGetLastError();
 }
 
