@@ -149,7 +149,7 @@ int p2p_attn_probs(const p2p_attn_tensors* t, const uint8_t* key_mask, float* pr
   if (!probs) return P2P_E_ARG;
   SelfArgs a;
   fill_common(a, t);
-  a.variant = 0;
+  a.variant = self_variant();
   a.lse = nullptr;
   a.probs = nullptr;
   a.key_mask = key_mask;

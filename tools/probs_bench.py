@@ -36,10 +36,14 @@ def main():
         o = torch.empty_like(q)
         probs = torch.empty(N * H, P, P, device="cuda")
         t_p = timeit(lambda: _hip.attn_probs(q, k, H, d ** -0.5, probs))
+        os.environ["P2P_SELF_VARIANT"] = "7"
+        t_nt = timeit(  # P2P_SELF_VARIANT=7: plain (temporal) stores
+            lambda: _hip.attn_probs(q, k, H, d ** -0.5, probs))
+        os.environ["P2P_SELF_VARIANT"] = "0"
         t_v = timeit(lambda: _hip.attn_pv(probs, v, o, H))
         nbytes = probs.numel() * 4
         print(json.dumps({"P": P, "d": d, "probs_us": round(t_p, 1), "probs_GBps": round(nbytes / t_p / 1e3, 1),
-                          "pv_us": round(t_v, 1), "pv_GBps": round(nbytes / t_v / 1e3, 1),
+                          "probs_plain_store_us": round(t_nt, 1), "pv_us": round(t_v, 1), "pv_GBps": round(nbytes / t_v / 1e3, 1),
                           "probs_MB": round(nbytes / 1e6, 1)}), flush=True)
         del probs
         torch.cuda.empty_cache()
