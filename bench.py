@@ -14,6 +14,7 @@ at the end of the timed region.  Prints one JSON line (rank 0).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -78,10 +79,12 @@ def pmc_traffic():
     return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(num_ddim_steps: int):
-    """The oracle's fp32 CPU restatement of the same workload on the host cores: ONE denoising
-    step (U-Net at batch 8 with the eager patched attention + reference controller +
-    LocalBlend + DDIM), extrapolated to the 50-step group."""
+def cpu_baseline(num_ddim_steps: int, sample_steps: int = 2):
+    """The oracle's fp32 CPU restatement of the same workload on the host cores -- the reference
+    itself is not importable here (no diffusers), so this is the port: ``sample_steps``
+    consecutive denoising steps (U-Net at batch 8 with the eager patched attention + reference
+    controller + LocalBlend + DDIM) timed and extrapolated x(num_ddim_steps / sample_steps)
+    to the 50-step group (2 steps x 25)."""
     from oracle import control as oc
     from oracle import forward as ofw
     from p2p_amd import pipeline as pl
@@ -99,51 +102,80 @@ def cpu_baseline(num_ddim_steps: int):
     ctx = torch.cat([model.text_encoder(uids)[0], model.text_encoder(ids)[0]])
     lat = pl.seed_latent(0).expand(4, 4, 64, 64).clone()
     model.scheduler.set_timesteps(num_ddim_steps)
-    t = model.scheduler.timesteps[0]
     with torch.no_grad():
         t0 = time.perf_counter()
-        eps = model.unet(torch.cat([lat] * 2), t, encoder_hidden_states=ctx)["sample"]
-        eu, ec = eps.chunk(2)
-        lat = model.scheduler.step(eu + 7.5 * (ec - eu), t, lat)["prev_sample"]
-        lat = ctrl.step_callback(lat)
+        for t in model.scheduler.timesteps[:sample_steps]:
+            eps = model.unet(torch.cat([lat] * 2), t, encoder_hidden_states=ctx)["sample"]
+            eu, ec = eps.chunk(2)
+            lat = model.scheduler.step(eu + 7.5 * (ec - eu), t, lat)["prev_sample"]
+            lat = ctrl.step_callback(lat)
         dt = time.perf_counter() - t0
-    per_group = dt * num_ddim_steps
+    per_group = dt / sample_steps * num_ddim_steps
     return {"value": 1.0 / per_group, "unit": "edit-groups/s", "cores": cores, "kind": "port",
-            "sample": f"1 of {num_ddim_steps} DDIM steps (U-Net N=8 fp32 + oracle eager attention/edits/"
-                      f"store + LocalBlend + DDIM) timed = {dt:.2f} s, x{num_ddim_steps} extrapolated"}
+            "sample": f"{sample_steps} of {num_ddim_steps} DDIM steps timed = {dt:.2f} s, "
+                      f"x{num_ddim_steps / sample_steps:g} extrapolated; oracle port (fp32 torch on the host: "
+                      f"U-Net N=8 + eager attention + reference controller/store + LocalBlend + DDIM) -- the "
+                      f"reference itself is not importable here (no diffusers)"}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3, help="edit groups timed per rank")
+    ap.add_argument("--steps", type=int, default=3, help="batches of --groups-per-call edit groups timed per rank")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--unet-dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--compute", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--groups-per-call", type=int, default=1,
-                    help="edit groups denoised per U-Net call (controllers.GroupBatch; a step = one such\n                         batch); 1 = configs[1] as quoted")
+                    help="edit groups denoised per U-Net call (controllers.GroupBatch; a step = one such\n"
+                         "batch); 1 = configs[1] as quoted")
+    ap.add_argument("--seeds", type=int, default=0,
+                    help="configs[3] sweep: time ALL of seeds 0..S-1, partitioned over the ranks and run\n"
+                         "--groups-per-call at a time (--steps is then ignored); value = S / wall")
     ap.add_argument("--store-self", action="store_true",
-                    help="also keep the 32x32/16x16/8x8 SELF maps (main.py AttentionStore default); the\n                         north-star workload keeps only the maps AttentionStore/LocalBlend read")
+                    help="also keep the 32x32/16x16/8x8 SELF maps (main.py AttentionStore default); the\n"
+                         "north-star workload keeps only the maps AttentionStore/LocalBlend read")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start torchrun as a CHILD before anything touches the GPU (never
+        # exec from a process that may have), wait, and exit with its status
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(cmd, env=env))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} launched with WORLD_SIZE={world}")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from p2p_amd import _hip, config
+    from p2p_amd import _hip, config, controllers, sweep
     from p2p_amd import pipeline as pl
     config.set_compute(args.compute)
     _hip.lib()
+    _hip.check_source_hash()
 
     dtype = torch.bfloat16 if args.unet_dtype == "bf16" else torch.float32
     model = pl.SyntheticStableDiffusion(device=dev, dtype=dtype)
     prompts = pl.north_star_prompts()
+    B = len(prompts)
     timer = DominantKernelTimer()
     _hip.LAUNCH_OBSERVER = timer
 
@@ -153,31 +185,42 @@ def main():
         return pl.make_replace_controller(prompts, args.ddim_steps, device=dev, store_self_maps=args.store_self)
 
     def batch(seeds):
-        # one step: G edit groups (each 1 source + 3 edits, its own seed), one U-Net call per DDIM step
-        if G == 1:
-            return pl.run_edit_group(model, prompts, make_ctrl(), pl.seed_latent(seeds[0]),
-                                     num_steps=args.ddim_steps)[None]
-        from p2p_amd import controllers
-        ctrl = controllers.GroupBatch([make_ctrl() for _ in seeds])
-        lat = pl.run_edit_groups(model, [prompts] * G, ctrl, [pl.seed_latent(s) for s in seeds],
+        """One step: len(seeds) <= G edit groups (each 1 source + 3 edits, its own seed), one U-Net
+        call per DDIM step.  Returns the final latents [g, B, 4, 64, 64] and each group's reduced
+        stored maps [g, B, 16, 16, 77] (aggregate_attention's 16x16 cross average per prompt)."""
+        if len(seeds) == 1:
+            ctrl = make_ctrl()
+            lat = pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(seeds[0]), num_steps=args.ddim_steps)
+            maps = controllers.reduce_maps(ctrl, 16, ["up", "down"], True, B)
+            return lat[None], maps[None]
+        members = [make_ctrl() for _ in seeds]
+        ctrl = controllers.GroupBatch(members)
+        lat = pl.run_edit_groups(model, [prompts] * len(seeds), ctrl, [pl.seed_latent(s) for s in seeds],
                                  num_steps=args.ddim_steps)
-        return lat.reshape(G, len(prompts), *lat.shape[1:])
+        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in members])
+        return lat.reshape(len(seeds), B, *lat.shape[1:]), maps
 
     # groups (seeds) partitioned across ranks round-robin: no collective on the data path
-    from p2p_amd import sweep
-    all_seeds = list(range(world * (args.warmup + args.steps) * G))
+    if args.seeds > 0:
+        all_seeds = list(range(args.seeds))
+        warm_seeds = [10 ** 6 + i for i in range(args.warmup * G)]
+    else:
+        all_seeds = list(range(world * args.steps * G))
+        warm_seeds = [10 ** 6 + rank * args.warmup * G + i for i in range(args.warmup * G)]
     mine = sweep.partition(all_seeds, rank, world)
-    batches = [mine[i * G:(i + 1) * G] for i in range(args.warmup + args.steps)]
-    for b in batches[:args.warmup]:
-        batch(b)
+    timed = [mine[i:i + G] for i in range(0, len(mine), G)]
+    for i in range(args.warmup):
+        batch(warm_seeds[i * G:(i + 1) * G])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timer.enabled = True
     t0 = time.perf_counter()
-    finals = torch.cat([batch(b) for b in batches[args.warmup:]]).float()   # [steps * G, 4, 4, 64, 64]
-    # one RCCL all-gather of the final latents at the end (the only inter-GPU traffic)
-    gathered = sweep.gather_latents(finals, world * args.steps * G, world)
+    outs = [batch(b) for b in timed]
+    lats = torch.cat([o[0] for o in outs]).float() if outs else torch.zeros(0, B, 4, 64, 64, device=dev)
+    maps = torch.cat([o[1] for o in outs]).float() if outs else torch.zeros(0, B, 16, 16, 77, device=dev)
+    # ONE RCCL all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
+    lat_all, maps_all = sweep.gather_results([lats, maps], len(all_seeds), world)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -187,7 +230,11 @@ def main():
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
-    assert gathered.shape[0] == world * args.steps * G and torch.isfinite(gathered).all()
+    n_total = len(all_seeds)
+    assert lat_all.shape == (n_total, B, 4, 64, 64) and maps_all.shape == (n_total, B, 16, 16, 77)
+    assert torch.isfinite(lat_all).all() and torch.isfinite(maps_all).all()
+    # each source prompt's gathered map row is an average of probability rows: it sums to 1
+    assert (maps_all[:, 0].sum(-1) - 1).abs().max().item() < 1e-2
 
     avg_ms, flops, n_launch = timer.summary()
     if rank == 0:
@@ -204,16 +251,20 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.ddim_steps)
-        total = world * args.steps * G
+        n_steps = max(1, (len(sweep.partition(all_seeds, 0, world)) + G - 1) // G)
+        workload = ("configs[3]: seed sweep of " + str(n_total) + " edit groups, " if args.seeds > 0 else
+                    "configs[1]: ")
         line = {
             "metric": "edit-groups/sec (src+3 edits, SD1.4 512², 50 DDIM)",
-            "value": total / elapsed, "unit": "edit-groups/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.compute,
+            "value": n_total / elapsed, "unit": "edit-groups/s", "n_gpus": world, "steps": n_steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / n_steps, "higher_is_better": True,
+            "scaling": "weak" if args.seeds == 0 else "strong", "vs_baseline": None, "dtype": args.compute,
             "data": "synthetic (random-init SD-v1.4-shaped U-Net, seeded x_T, stand-in text context)",
-            "config": {"workload": "configs[1]: SD-v1.4 512x512 AttentionReplace + LocalBlend, 1 source + 3 edits, "
-                                   f"{args.ddim_steps} DDIM, CFG 7.5", "global_batch": 8 * G * world, "groups_per_call": G,
-                       "unet_dtype": args.unet_dtype, "self_maps_kept": args.store_self, "parallelism": f"replicas x{world} (groups by seed)"},
+            "config": {"workload": workload + "SD-v1.4 512x512 AttentionReplace + LocalBlend, 1 source + 3 edits, "
+                                   f"{args.ddim_steps} DDIM, CFG 7.5", "global_batch": 8 * G * world,
+                       "groups_per_call": G, "groups_total": n_total, "unet_dtype": args.unet_dtype,
+                       "self_maps_kept": args.store_self, "gathered": "final latents + 16x16 cross maps (1 all-gather)",
+                       "parallelism": f"replicas x{world} (groups by seed)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))

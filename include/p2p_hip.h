@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 9
+#define P2P_ABI_VERSION 10
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -103,7 +103,9 @@ typedef struct {
   int32_t count;
   const void* program;
   const float* alpha;
-  int32_t flags; /* P2P_PROGRAM_F_* of program (host-known: sizes the launch's LDS) */
+  int32_t flags;   /* P2P_PROGRAM_F_* of program (host-known: sizes the launch's LDS) */
+  int32_t n_edits; /* edit records the program holds (its header[0]); a group with
+                      count - 1 > n_edits is rejected (P2P_E_BATCH) before any launch */
 } p2p_group;
 
 /* Cross-attention (ptp_utils.py:183-208 with context=...) with the controller's cross edit
@@ -205,8 +207,10 @@ int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream);
  * reference's cuda:0 device. */
 int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream);
 
-/* Build/runtime information. */
+/* Build/runtime information.  p2p_source_hash: content hash of the HIP sources the library
+ * was built from (p2p_amd/_srchash.py), so a host can refuse a stale prebuilt binary. */
 int p2p_abi_version(void);
+const char* p2p_source_hash(void);
 const char* p2p_error_string(int code);
 
 #ifdef __cplusplus

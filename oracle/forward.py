@@ -17,6 +17,9 @@ def eager_attention(module, x, context, controller, place):
     v = module.to_v(src)
 
     def split(t):
+        # the attention math always runs in fp32 (the reference's model dtype, main.py:29): a bf16
+        # U-Net's projections are upcast here and the result cast back before to_out
+        t = t.float()
         return t.reshape(b, t.shape[1], H, t.shape[2] // H).permute(0, 2, 1, 3).reshape(b * H, t.shape[1], -1)
 
     q, k, v = split(q), split(k), split(v)
@@ -24,7 +27,7 @@ def eager_attention(module, x, context, controller, place):
     if controller is not None:
         attn = controller(attn, is_cross, place)
     out = torch.einsum("bij,bjd->bid", attn, v)
-    out = out.reshape(b, H, n, -1).permute(0, 2, 1, 3).reshape(b, n, -1)
+    out = out.reshape(b, H, n, -1).permute(0, 2, 1, 3).reshape(b, n, -1).to(x.dtype)
     to_out = module.to_out[0] if isinstance(module.to_out, torch.nn.ModuleList) else module.to_out
     return to_out(out)
 

@@ -47,16 +47,30 @@ void fill_common(A& a, const p2p_attn_tensors* t) {
   no_maps(a);
 }
 
-int self_variant() {
-  const char* e = getenv("P2P_SELF_VARIANT");  // read per call: in-process A/B timing
+// Kernel variants for A/B timing (tools/self_variants.py): honoured only by a library built with
+// `make EXPERIMENTS=1`, and read once at load -- a production library always runs the default
+// kernels whatever the environment says.
+#ifdef P2P_EXPERIMENTS
+const int kSelfVariant = [] {
+  const char* e = getenv("P2P_SELF_VARIANT");
   return e ? atoi(e) : 0;
-}
+}();
+#else
+constexpr int kSelfVariant = 0;
+#endif
+int self_variant() { return kSelfVariant; }
+
+#ifndef P2P_SOURCE_HASH
+#define P2P_SOURCE_HASH "unstamped"
+#endif
 
 }  // namespace
 
 extern "C" {
 
 int p2p_abi_version(void) { return P2P_ABI_VERSION; }
+
+const char* p2p_source_hash(void) { return P2P_SOURCE_HASH; }
 
 const char* p2p_error_string(int code) {
   switch (code) {
@@ -114,6 +128,9 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     const p2p_group& G = groups[g];
     if (G.first < 0 || G.count < 1 || G.first + G.count > t->n_batch) return P2P_E_BATCH;
     if (G.program && G.count > 1 && !G.alpha) return P2P_E_ARG;
+    // the kernel reads edit record / dense tile / alpha row b - 1 for b < count: a program built
+    // for fewer edits than the group has would be read past its end
+    if (G.program && G.count - 1 > G.n_edits) return P2P_E_BATCH;
     a.grp_first[g] = G.first;
     a.grp_count[g] = G.count;
     a.grp_prog[g] = G.program;

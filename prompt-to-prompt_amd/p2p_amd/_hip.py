@@ -27,7 +27,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class HipError(RuntimeError):
@@ -50,7 +50,8 @@ class AttnTensors(ctypes.Structure):
 
 class Group(ctypes.Structure):
     _fields_ = [("first", ctypes.c_int32), ("count", ctypes.c_int32),
-                ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+                ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p), ("flags", ctypes.c_int32),
+                ("n_edits", ctypes.c_int32)]
 
 
 class BlendArgs(ctypes.Structure):
@@ -89,6 +90,7 @@ def lib():
         i32, vp, f32, i64 = ctypes.c_int32, ctypes.c_void_p, ctypes.c_float, ctypes.c_int64
         L.p2p_abi_version.restype = ctypes.c_int
         L.p2p_error_string.restype = ctypes.c_char_p
+        L.p2p_source_hash.restype = ctypes.c_char_p
         L.p2p_error_string.argtypes = [ctypes.c_int]
         L.p2p_self_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, i32, vp, vp]
         L.p2p_cross_attn_fwd.argtypes = [ctypes.POINTER(AttnTensors), vp, i32, vp, vp, i32, vp]
@@ -110,7 +112,20 @@ def lib():
     return _lib
 
 
-EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
+def check_source_hash() -> str:
+    """Raise unless the loaded library was built from the HIP sources in this tree (the Makefile
+    stamps _srchash.source_hash() into it).  smoke() and the GPU tests call this, so a stale
+    prebuilt libp2p_hip.so cannot pass for the current sources."""
+    from . import _srchash
+    built = lib().p2p_source_hash().decode()
+    tree = _srchash.source_hash()
+    if built != tree:
+        raise HipError(f"libp2p_hip.so was built from sources {built}, the tree has {tree}: rebuild "
+                       f"(make -C prompt-to-prompt_amd/csrc)")
+    return built
+
+
+EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_source_hash", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
                     "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step",
                     "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace")
 
@@ -177,21 +192,12 @@ def _i32_array(vals: Sequence[int]):
     return arr
 
 
-_LSE_WS = {}
-
-
 def _lse_workspace(device, numel):
-    """Per-device f32 scratch for the row log-sum-exp of a self launch that keeps maps (grown,
-    never shrunk; stream-ordered reuse: every launch on the device's current stream).  Under
-    hipGraph capture a call-local buffer from the graph's private pool is used instead, so a
-    replay never shares the scratch with eager launches."""
-    if torch.cuda.is_current_stream_capturing():
-        return torch.empty(numel, dtype=torch.float32, device=device)
-    buf = _LSE_WS.get(device)
-    if buf is None or buf.numel() < numel:
-        buf = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
-        _LSE_WS[device] = buf
-    return buf
+    """f32 scratch for the row log-sum-exp of a self launch that keeps maps: allocated per call
+    from torch's caching allocator on the current stream (cheap), so launches on different
+    streams -- or replays of a captured graph -- never share it; the allocator's stream
+    ordering keeps it alive until the launch that reads it has run."""
+    return torch.empty(numel, dtype=torch.float32, device=device)
 
 
 def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None, store_slot=None,
@@ -225,6 +231,7 @@ def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, sto
         G[i].program = prog.data_ptr() if prog is not None else None
         G[i].alpha = alpha.data_ptr() if alpha is not None else None
         G[i].flags = int(getattr(prog, "p2p_flags", 0)) if prog is not None else 0
+        G[i].n_edits = int(getattr(prog, "p2p_n_edits", 0)) if prog is not None else 0
     slots = _i32_array(store_slot) if store_slot is not None else None
     if store is not None:
         _require_cuda(store)

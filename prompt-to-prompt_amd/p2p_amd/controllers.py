@@ -559,11 +559,17 @@ class GroupBatch(AttentionControl):
         for m in self.members:
             if not (isinstance(m, AttentionControl) and m.fused_supported()):
                 raise ValueError(f"{type(m).__name__}: GroupBatch members must take the fused kernel path")
+            # an edit controller's tables (program records, alpha rows, LocalBlend slices) are
+            # sized by its own prompt count: it must equal the group size the kernels get
+            if isinstance(m, AttentionControlEdit) and m.batch_size != self.group_size:
+                raise ValueError(f"{type(m).__name__} was built for {m.batch_size} prompts, "
+                                 f"GroupBatch groups have {self.group_size}")
         storing = {isinstance(m, AttentionStore) for m in self.members}
         if len(storing) != 1:
             raise ValueError("mix of storing and non-storing controllers")
         self._storing = storing.pop()
-        self._store_self = self._storing and all(m.store_self_maps for m in self.members)
+        if self._storing and len({bool(m.store_self_maps) for m in self.members}) != 1:
+            raise ValueError("GroupBatch members disagree on store_self_maps")
         self._calls = defaultdict(int)
         self._combined = defaultdict(list)
 
@@ -630,7 +636,10 @@ class GroupBatch(AttentionControl):
         if N != 2 * GB:
             raise ValueError(f"GroupBatch of {G} x {B} prompts got a U-Net batch of {N}")
         store, acc, slots = None, False, None
-        if self._storing and P <= MAX_STORED_QUERIES and (is_cross or self._store_self):
+        store_self = self._storing and all(m.store_self_maps for m in self.members)
+        if self._storing and not is_cross and any(m.store_self_maps for m in self.members) and not store_self:
+            raise ValueError("GroupBatch members disagree on store_self_maps")
+        if self._storing and P <= MAX_STORED_QUERIES and (is_cross or store_self):
             key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
             idx = self._calls[key]
             self._calls[key] = idx + 1
@@ -697,8 +706,10 @@ def get_equalizer(text: str, word_select: Union[int, Tuple[int, ...]],
 def aggregate_attention(attention_store: AttentionStore, res: int, from_where: List[str], is_cross: bool,
                         select: int, prompts: Optional[List[str]] = None):
     """main.py:293-307 (``prompts`` is the reference's module global; defaults to the
-    controller's batch size)."""
-    n_prompts = len(prompts) if prompts is not None else attention_store.batch_size
+    controller's batch size -- a plain AttentionStore has none, so pass ``prompts=`` there)."""
+    n_prompts = len(prompts) if prompts is not None else getattr(attention_store, "batch_size", None)
+    if n_prompts is None:
+        raise ValueError(f"{type(attention_store).__name__} does not know its prompt count: pass prompts=")
     maps = attention_store.get_average_attention()
     picked = []
     for location in from_where:
@@ -707,3 +718,20 @@ def aggregate_attention(attention_store: AttentionStore, res: int, from_where: L
                 picked.append(item.reshape(n_prompts, -1, res, res, item.shape[-1])[select])
     out = torch.cat(picked, dim=0)
     return (out.sum(0) / out.shape[0]).cpu()
+
+
+def reduce_maps(attention_store: AttentionStore, res: int, from_where: List[str], is_cross: bool,
+                n_prompts: int) -> torch.Tensor:
+    """aggregate_attention for every prompt at once, left on the device: the average over the
+    stored layers at ``res`` and their heads of the step-averaged maps, [n_prompts, res, res, K]
+    (main.py:296-307 with ``select`` = each prompt in turn; same sum order per prompt)."""
+    maps = attention_store.get_average_attention()
+    picked = []
+    for location in from_where:
+        for item in maps[f"{location}_{'cross' if is_cross else 'self'}"]:
+            if item.shape[1] == res ** 2:
+                picked.append(item.reshape(n_prompts, -1, res, res, item.shape[-1]))
+    if not picked:
+        raise ValueError(f"no stored {'cross' if is_cross else 'self'} maps at {res}x{res} in {from_where}")
+    out = torch.cat(picked, dim=1)
+    return out.sum(1) / out.shape[1]

@@ -99,6 +99,7 @@ class EditProgram:
         blob = self.blob()
         t = torch.from_numpy(blob.copy()).to(device)
         t.p2p_flags = F_DENSE if int(blob[16:20].view(np.int32)[0]) else 0   # p2p_group.flags
+        t.p2p_n_edits = self.n_edits                                          # p2p_group.n_edits
         return t
 
 

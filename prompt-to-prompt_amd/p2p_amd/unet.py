@@ -146,9 +146,10 @@ class Upsample2D(nn.Module):
 
 
 class CrossAttnDownBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, layers=2, heads=8, context_dim=768, downsample=True):
+    def __init__(self, in_ch, out_ch, layers=2, heads=8, context_dim=768, downsample=True, temb_ch=1280):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch) for i in range(layers)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb_ch)
+                                      for i in range(layers)])
         self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, context_dim)
                                          for _ in range(layers)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if downsample else None
@@ -165,9 +166,10 @@ class CrossAttnDownBlock2D(nn.Module):
 
 
 class DownBlock2D(nn.Module):
-    def __init__(self, in_ch, out_ch, layers=2, downsample=False):
+    def __init__(self, in_ch, out_ch, layers=2, downsample=False, temb_ch=1280):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch) for i in range(layers)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(in_ch if i == 0 else out_ch, out_ch, temb_ch)
+                                      for i in range(layers)])
         self.downsamplers = nn.ModuleList([Downsample2D(out_ch)]) if downsample else None
 
     def forward(self, x, temb, ctx=None):
@@ -181,19 +183,19 @@ class DownBlock2D(nn.Module):
         return x, outs
 
 
-def _up_resnets(in_ch, prev_ch, out_ch, layers):
+def _up_resnets(in_ch, prev_ch, out_ch, layers, temb_ch=1280):
     mods = []
     for i in range(layers):
         skip = in_ch if i == layers - 1 else out_ch
         r_in = prev_ch if i == 0 else out_ch
-        mods.append(ResnetBlock2D(r_in + skip, out_ch))
+        mods.append(ResnetBlock2D(r_in + skip, out_ch, temb_ch))
     return nn.ModuleList(mods)
 
 
 class UpBlock2D(nn.Module):
-    def __init__(self, in_ch, prev_ch, out_ch, layers=3, upsample=True):
+    def __init__(self, in_ch, prev_ch, out_ch, layers=3, upsample=True, temb_ch=1280):
         super().__init__()
-        self.resnets = _up_resnets(in_ch, prev_ch, out_ch, layers)
+        self.resnets = _up_resnets(in_ch, prev_ch, out_ch, layers, temb_ch)
         self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if upsample else None
 
     def forward(self, x, temb, skips, ctx=None):
@@ -206,9 +208,9 @@ class UpBlock2D(nn.Module):
 
 
 class CrossAttnUpBlock2D(nn.Module):
-    def __init__(self, in_ch, prev_ch, out_ch, layers=3, heads=8, context_dim=768, upsample=True):
+    def __init__(self, in_ch, prev_ch, out_ch, layers=3, heads=8, context_dim=768, upsample=True, temb_ch=1280):
         super().__init__()
-        self.resnets = _up_resnets(in_ch, prev_ch, out_ch, layers)
+        self.resnets = _up_resnets(in_ch, prev_ch, out_ch, layers, temb_ch)
         self.attentions = nn.ModuleList([Transformer2DModel(heads, out_ch // heads, out_ch, context_dim)
                                          for _ in range(layers)])
         self.upsamplers = nn.ModuleList([Upsample2D(out_ch)]) if upsample else None
@@ -224,9 +226,9 @@ class CrossAttnUpBlock2D(nn.Module):
 
 
 class UNetMidBlock2DCrossAttn(nn.Module):
-    def __init__(self, ch, heads=8, context_dim=768):
+    def __init__(self, ch, heads=8, context_dim=768, temb_ch=1280):
         super().__init__()
-        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch), ResnetBlock2D(ch, ch)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb_ch), ResnetBlock2D(ch, ch, temb_ch)])
         self.attentions = nn.ModuleList([Transformer2DModel(heads, ch // heads, ch, context_dim)])
 
     def forward(self, x, temb, ctx):
@@ -268,11 +270,11 @@ class UNet2DConditionModel(nn.Module):
             in_ch, out_ch = out_ch, boc[i]
             last = i == len(boc) - 1
             if last:
-                self.down_blocks.append(DownBlock2D(in_ch, out_ch, layers_per_block, downsample=False))
+                self.down_blocks.append(DownBlock2D(in_ch, out_ch, layers_per_block, downsample=False, temb_ch=temb))
             else:
                 self.down_blocks.append(CrossAttnDownBlock2D(in_ch, out_ch, layers_per_block, heads,
-                                                             cross_attention_dim, downsample=True))
-        self.mid_block = UNetMidBlock2DCrossAttn(boc[-1], heads, cross_attention_dim)
+                                                             cross_attention_dim, downsample=True, temb_ch=temb))
+        self.mid_block = UNetMidBlock2DCrossAttn(boc[-1], heads, cross_attention_dim, temb_ch=temb)
         self.up_blocks = nn.ModuleList()
         rev = boc[::-1]
         out_ch = rev[0]
@@ -281,10 +283,11 @@ class UNet2DConditionModel(nn.Module):
             in_ch = rev[min(i + 1, len(rev) - 1)]
             last = i == len(rev) - 1
             if i == 0:
-                self.up_blocks.append(UpBlock2D(in_ch, prev, out_ch, layers_per_block + 1, upsample=True))
+                self.up_blocks.append(UpBlock2D(in_ch, prev, out_ch, layers_per_block + 1, upsample=True,
+                                                temb_ch=temb))
             else:
                 self.up_blocks.append(CrossAttnUpBlock2D(in_ch, prev, out_ch, layers_per_block + 1, heads,
-                                                         cross_attention_dim, upsample=not last))
+                                                         cross_attention_dim, upsample=not last, temb_ch=temb))
         self.conv_norm_out = nn.GroupNorm(32, boc[0], eps=1e-5)
         self.conv_out = nn.Conv2d(boc[0], out_channels, 3, padding=1)
 

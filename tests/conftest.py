@@ -34,7 +34,12 @@ def tok():
 
 @pytest.fixture(scope="session")
 def cuda():
+    """Every -m gpu test takes this fixture.  No visible GPU is a FAILURE, not a skip: a GPU run
+    whose device vanished must not exit 0 (the CPU suite deselects these tests with -m "not gpu")."""
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("no GPU visible to a -m gpu test (torch.cuda.is_available() is False)")
+    from p2p_amd import _hip
+    _hip.lib()
+    _hip.check_source_hash()     # the loaded libp2p_hip.so was built from THIS tree
     return torch.device("cuda:0")

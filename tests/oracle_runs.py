@@ -1,0 +1,68 @@
+"""Whole edit groups through the ORACLE (test infrastructure, never the product): the same
+U-Net weights and seed as a product run, every patched CrossAttention replaced by the oracle's
+eager fp32 attention + reference controller semantics, the oracle's DDIM step and LocalBlend,
+in a plain loop that restates ptp_utils.py:65-76 and :129-172."""
+from __future__ import annotations
+
+import torch
+
+from oracle import control as oc
+from oracle import forward as ofw
+from oracle import tables as otab
+from p2p_amd import pipeline as pl
+
+
+def oracle_controller(kind, prompts, tok, steps, dev, local_blend=None, flavour="null", cross=0.8,
+                      self_steps=0.4, word="mountain", value=2.0):
+    """kind "replace" (configs[1]: null_text AttentionReplace) or "refine_reweight" (configs[2]:
+    main.py AttentionReweight(equalizer) chained on AttentionRefine, pl.make_refine_reweight_controller)."""
+    if kind == "replace":
+        c = oc.OracleController(flavour, "replace", prompts, steps, cross, self_steps, tok, local_blend=local_blend,
+                                store_self=False)
+        c.mapper, c.alpha = c.mapper.to(dev), c.alpha.to(dev)
+        return c
+    inner = oc.OracleController("main", "refine", prompts, steps, cross, self_steps, tok)
+    inner.mapper, inner.ref_alphas, inner.alpha = inner.mapper.to(dev), inner.ref_alphas.to(dev), inner.alpha.to(dev)
+    eq = otab.equalizer_main(prompts[0], (word,), (value,), tok)
+    c = oc.OracleController("main", "reweight", prompts, steps, cross, self_steps, tok, equalizer=eq.to(dev),
+                            inner=inner, local_blend=local_blend, store_self=False)
+    c.alpha = c.alpha.to(dev)
+    return c
+
+
+def oracle_group(model, prompts, x_T, ctrl, steps=50, guidance=7.5):
+    """Final latents [B, 4, h, w] f32 of one edit group; ``ctrl`` (an OracleController) keeps the
+    running-sum store.  x_T: [1, 4, h, w] (init_latent, ptp_utils.py:88-95)."""
+    dev = model.device
+    ofw.install(model, ctrl)
+    B = len(prompts)
+    ids = model.tokenizer(prompts, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    uids = model.tokenizer([""] * B, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
+    ctx = torch.cat([model.text_encoder(uids)[0], model.text_encoder(ids)[0]]).to(next(model.unet.parameters()).dtype)
+    lat = x_T.expand(B, *x_T.shape[1:]).to(dev).float()
+    sched = model.scheduler
+    sched.set_timesteps(steps)
+    ac = sched.alphas_cumprod.to(dev)
+    udt = next(model.unet.parameters()).dtype
+    with torch.no_grad():
+        for t in sched.timesteps:
+            eps = model.unet(torch.cat([lat] * 2).to(udt), t, encoder_hidden_states=ctx)["sample"].float()
+            eu, ec = eps.chunk(2)
+            lat = oc.ddim_prev(ac, ac[0], eu + guidance * (ec - eu), int(t), lat)
+            lat = ctrl.step_callback(lat)
+    return lat
+
+
+def replace_group(model, prompts, x_T, tok, steps=50, blend=True):
+    """configs[1] through the oracle: AttentionReplace + null_text LocalBlend (make_replace_controller)."""
+    # start_blend = int(0.2 * NUM_DDIM_STEPS) with the module constant 50, whatever the step count
+    lb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok) if blend else None
+    if lb is not None:
+        lb.alpha = lb.alpha.to(model.device)
+    ctrl = oracle_controller("replace", prompts, tok, steps, model.device, local_blend=lb)
+    return oracle_group(model, prompts, x_T, ctrl, steps), ctrl, lb
+
+
+def cosine(a, b):
+    a, b = a.flatten(1).double(), b.flatten(1).double()
+    return torch.nn.functional.cosine_similarity(a, b, dim=1)

@@ -101,3 +101,30 @@ def test_localblend_rejects():
     a = _hip.BlendArgs()
     assert L.p2p_localblend(ctypes.byref(a), None) == -1
     assert L.p2p_store_scale(None, None, 1.0, 10, None) == -1
+
+
+def test_cross_attn_rejects_program_with_too_few_edits():
+    """a group of 4 prompts needs a program with >= 3 edit records; one built for fewer
+    would make the kernel read past the program blob and the alpha row."""
+    L = _hip.lib()
+    t = _tensors(n_key=77)
+    G = (_hip.Group * 2)()
+    G[0].first, G[0].count = 0, 4
+    G[1].first, G[1].count = 4, 4
+    G[1].program, G[1].alpha, G[1].n_edits = 64, 128, 2
+    assert L.p2p_cross_attn_fwd(ctypes.byref(t), G, 2, None, None, 0, None) == -5
+
+
+def test_library_built_from_this_tree():
+    """The Makefile stamps the source hash; a stale prebuilt library fails this check."""
+    from p2p_amd import _srchash
+    assert _hip.lib().p2p_source_hash().decode() == _srchash.source_hash()
+    assert _hip.check_source_hash() == _srchash.source_hash()
+
+
+def test_production_library_ignores_variant_env(monkeypatch):
+    """kernel variants are an experiments-build feature read once at load; the
+    production build never reads P2P_SELF_VARIANT (its getenv is compiled out)."""
+    import subprocess
+    out = subprocess.run(["strings", _hip.library_path()], capture_output=True, text=True).stdout
+    assert "P2P_SELF_VARIANT" not in out

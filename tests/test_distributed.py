@@ -1,7 +1,15 @@
-"""Multi-rank sweep path on CPU (gloo, world size 2 and 3): seed sharding and the final
-all-gather must reproduce the single-process sweep exactly."""
+"""Multi-rank sweep path on CPU (gloo, world size 2 and 3): seed sharding and the ONE final
+all-gather of latents + reduced maps must reproduce the single-process sweep exactly.
+
+The edit group each rank runs is a real (tiny) one: an SD-topology U-Net with small channels and
+a 32x32 latent, denoised with the oracle's eager attention + AttentionReplace controller + DDIM
+(the product's kernels need a GPU); its result is the final latents and the store's reduced
+16x16 cross maps (controllers.reduce_maps, aggregate_attention per prompt).  bench.py runs the
+same partition / gather code over RCCL with the product's HIP path.
+"""
 import os
 import socket
+from types import SimpleNamespace
 
 import pytest
 import torch
@@ -10,11 +18,36 @@ import torch.multiprocessing as mp
 
 from p2p_amd import sweep
 
+STEPS = 3
 
-def fake_group(seed: int) -> torch.Tensor:
-    """Stand-in for a 50-step edit group: a deterministic latent per seed ([4, 4, 8, 8])."""
+
+def tiny_model():
+    from p2p_amd.ddim import DDIMScheduler
+    from p2p_amd.pipeline import SyntheticTextEncoder
+    from p2p_amd.tokenizer import default_tokenizer
+    from p2p_amd.unet import UNet2DConditionModel
+    torch.manual_seed(0)
+    unet = UNet2DConditionModel(block_out_channels=(32, 64, 64, 64)).eval()
+    for p in unet.parameters():
+        p.requires_grad_(False)
+    return SimpleNamespace(tokenizer=default_tokenizer(), text_encoder=SyntheticTextEncoder(), unet=unet,
+                           scheduler=DDIMScheduler(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
+                                                   clip_sample=False, set_alpha_to_one=False),
+                           device=torch.device("cpu"))
+
+
+def real_group(model, seed: int):
+    """One 1-source + 3-edit AttentionReplace group, STEPS DDIM steps: (latents, reduced maps)."""
+    from oracle_runs import oracle_controller, oracle_group
+    from p2p_amd import controllers
+    from p2p_amd import pipeline as pl
+    prompts = pl.north_star_prompts()
+    ctrl = oracle_controller("replace", prompts, model.tokenizer, STEPS, model.device)
     g = torch.Generator().manual_seed(seed)
-    return torch.randn(4, 4, 8, 8, generator=g) * (1 + seed)
+    lat = oracle_group(model, prompts, torch.randn((1, 4, 32, 32), generator=g), ctrl, STEPS)
+    store = controllers.AttentionStore()               # the product's reduction over the oracle's store
+    store.attention_store, store.cur_step = ctrl.attention_store, ctrl.cur_step
+    return lat, controllers.reduce_maps(store, 16, ["up", "down"], True, len(prompts))
 
 
 def _free_port():
@@ -28,11 +61,13 @@ def _free_port():
 def _worker(rank, world, port, seeds, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        lat = sweep.run_sweep(seeds, fake_group, rank, world)
+        model = tiny_model()
+        lat, maps = sweep.run_sweep(seeds, lambda s: real_group(model, s), rank, world)
         if rank == 0:
-            torch.save(lat, out_path)
+            torch.save({"lat": lat, "maps": maps}, out_path)
     finally:
         dist.destroy_process_group()
 
@@ -44,12 +79,29 @@ def test_partition_round_robin():
     assert sorted(sum(parts, [])) == seeds
 
 
-@pytest.mark.parametrize("world,n", [(2, 6), (3, 7)])
-def test_gloo_sweep_matches_single_process(tmp_path, world, n):
+def test_gather_results_single_process_is_identity():
+    a, b = torch.randn(3, 4, 2), torch.randn(3, 5)
+    x, y = sweep.gather_results([a, b], 3, 1)
+    assert torch.equal(x, a) and torch.equal(y, b)
+
+
+@pytest.mark.parametrize("world,n", [(2, 3), (3, 4)])
+def test_gloo_sweep_real_groups_matches_single_process(tmp_path, world, n):
     seeds = [11 * i + 3 for i in range(n)]
-    out = str(tmp_path / "lat.pt")
+    out = str(tmp_path / "res.pt")
     mp.spawn(_worker, args=(world, _free_port(), seeds, out), nprocs=world, join=True)
     got = torch.load(out, weights_only=True)
-    want = sweep.run_sweep(seeds, fake_group)
-    assert got.shape == (n, 4, 4, 8, 8)
-    assert torch.equal(got, want)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(2)        # the workers' thread count: same CPU reduction order, same bits
+    try:
+        model = tiny_model()
+        want_lat, want_maps = sweep.run_sweep(seeds, lambda s: real_group(model, s))
+    finally:
+        torch.set_num_threads(threads)
+    assert got["lat"].shape == (n, 4, 4, 32, 32)
+    assert got["maps"].shape == (n, 4, 16, 16, 77)
+    assert torch.equal(got["lat"], want_lat.float())
+    assert torch.equal(got["maps"], want_maps.float())
+    # the source prompt's reduced maps are step/head/layer averages of probability rows (an edit's
+    # rows are P0 . M, whose mapper rows need not sum to 1 -- seq_aligner.py:180-183)
+    assert (got["maps"][:, 0].sum(-1) - 1).abs().max().item() < 1e-4

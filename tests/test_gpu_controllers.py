@@ -33,17 +33,18 @@ def calls(layers):
         yield place, True, P, 77, d
 
 
-def run_pair(prod, orc, layers, steps, tol_out, tol_store, x_t=None, seed=0, qscale=1.0):
+def run_pair(prod, orc, layers, steps, tol_out, tol_store, x_t=None, seed=0, qscale=1.0, prompts=None,
+             io_dtype=torch.float32):
     prod.num_att_layers = orc.num_att_layers = 2 * len(layers)
     g = torch.Generator(device="cuda").manual_seed(seed)
-    N = 2 * len(PROMPTS)
+    N = 2 * len(prompts if prompts is not None else PROMPTS)
     for step in range(steps):
         for place, is_cross, P, K, d in calls(layers):
             C = H * d
-            q = torch.randn(N, P, C, device="cuda", generator=g) * qscale
-            k = torch.randn(N, K, C, device="cuda", generator=g)
-            v = torch.randn(N, K, C, device="cuda", generator=g)
-            out = prod.attention(q, k, v, H, d ** -0.5, is_cross, place)
+            q = (torch.randn(N, P, C, device="cuda", generator=g) * qscale).to(io_dtype)
+            k = torch.randn(N, K, C, device="cuda", generator=g).to(io_dtype)
+            v = torch.randn(N, K, C, device="cuda", generator=g).to(io_dtype)
+            out = prod.attention(q, k, v, H, d ** -0.5, is_cross, place).float()
             probs = ref_probs(q, k, H, d ** -0.5).reshape(N * H, P, K)
             probs = orc(probs, is_cross, place)
             want = ref_out(probs.reshape(N, H, P, K), v, H)
@@ -107,13 +108,72 @@ def test_refine_reweight_store_self(cuda, tok, flavour):
         oinner.mapper = oinner.mapper.to(cuda)
         oinner.ref_alphas = oinner.ref_alphas.to(cuda)
         orc.equalizer = orc.equalizer.to(cuda)
-        global PROMPTS
-        saved = PROMPTS
-        PROMPTS = prompts
-        try:
-            run_pair(prod, orc, layers, 4, 5e-5, 4e-5, qscale=3.0)
-        finally:
-            PROMPTS = saved
+        run_pair(prod, orc, layers, 4, 5e-5, 4e-5, qscale=3.0, prompts=prompts)
+
+
+# The production edits in the production precision (bf16 MFMA kernels) at the SD geometries that
+# carry them -- G1 (P 4096, d 40: cross edit only, nothing stored), G2 (P 1024, d 80) and G3 (P 256,
+# d 160: self injection window, maps stored) -- at the config-2 batch (N = 8, H = 8), on peaky
+# rows (q x 8 / x 16: logits std 8-16) where a bf16 error in the probabilities would show, with
+# f32 inputs (split-bf16 Q.K^T, the f32-U-Net path) and bf16 inputs (the bf16 U-Net path).
+# Bars (north star): stored probabilities within 2e-3 per accumulated step; O within the bf16
+# PV bound 2^-7 max|V| (|V| <= ~5 here: 4e-2) -- main.py:233-278, null_text.py:290-349.
+EDIT_LAYERS = [("down", 4096, 40), ("down", 1024, 80), ("down", 256, 160)]
+REFINE_PROMPTS = ["a cat eating a burger", "a fluffy cat eating a burger", "a cat eating a burger at night",
+                  "a cat eating a big burger"]
+
+
+def _edit_pair(edit, tok, dev, steps):
+    """(prompts, product controller, oracle controller) for one production edit."""
+    if edit in ("refine", "reweight_refine"):
+        prompts = REFINE_PROMPTS
+    else:
+        prompts = PROMPTS
+    cross, selfw = {"default_": .8, "burger": .5}, (.0, .6)
+    oalpha_spec = dict(cross)
+    if edit == "refine":
+        prod = pc.AttentionRefine(prompts, steps, cross, selfw, tokenizer=tok, device=dev)
+        orc = oc.OracleController("main", "refine", prompts, steps, oalpha_spec, selfw, tok)
+        orc.mapper, orc.ref_alphas = orc.mapper.to(dev), orc.ref_alphas.to(dev)
+    else:
+        eq = pc.get_equalizer(prompts[0], "burger", (2.5,), tokenizer=tok)
+        oeq = otab.equalizer_main(prompts[0], "burger", (2.5,), tok).to(dev)
+        inner = oinner = None
+        if edit == "reweight_refine":
+            inner = pc.AttentionRefine(prompts, steps, cross, selfw, tokenizer=tok, device=dev)
+            oinner = oc.OracleController("main", "refine", prompts, steps, dict(cross), selfw, tok)
+            oinner.mapper, oinner.ref_alphas = oinner.mapper.to(dev), oinner.ref_alphas.to(dev)
+        elif edit == "reweight_replace":
+            inner = pc.AttentionReplace(prompts, steps, cross, selfw, tokenizer=tok, device=dev)
+            oinner = oc.OracleController("main", "replace", prompts, steps, dict(cross), selfw, tok)
+            oinner.mapper = oinner.mapper.to(dev)
+        if oinner is not None:
+            oinner.alpha = oinner.alpha.to(dev)
+        prod = pc.AttentionReweight(prompts, steps, cross, selfw, equalizer=eq, controller=inner, tokenizer=tok,
+                                    device=dev)
+        orc = oc.OracleController("main", "reweight", prompts, steps, oalpha_spec, selfw, tok, equalizer=oeq,
+                                  inner=oinner)
+    orc.alpha = orc.alpha.to(dev)
+    return prompts, prod, orc
+
+
+@pytest.mark.parametrize("io_dtype", [torch.float32, torch.bfloat16], ids=["f32in", "bf16in"])
+@pytest.mark.parametrize("qscale", [8.0, 16.0])
+@pytest.mark.parametrize("edit", ["refine", "reweight", "reweight_refine", "reweight_replace"])
+def test_edits_bf16_sd_geometry(cuda, tok, edit, qscale, io_dtype):
+    steps = 2
+    with config.compute_mode("bf16"):
+        prompts, prod, orc = _edit_pair(edit, tok, cuda, 10)
+        assert prod.fused_supported()
+        prog = prod._edit_program()
+        # the production edit path: every weight exact in bf16 -> the dense MFMA edit (R = P0 . M)
+        assert prog.dense_bf16() is not None
+        if edit == "refine":
+            assert (prog.c_rep != 0).any()          # the c_rep * P_b term of inserted words
+        if edit.startswith("reweight_"):
+            assert (prog.post != 1.0).any()         # the chained post-scale
+        run_pair(prod, orc, EDIT_LAYERS, steps, 4e-2, 2e-3 * steps, qscale=qscale, prompts=prompts,
+                 io_dtype=io_dtype, seed=int(qscale))
 
 
 def test_attention_store_only(cuda, tok):

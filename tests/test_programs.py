@@ -168,3 +168,37 @@ def test_program_too_many_terms_is_not_fused():
     m[0, :9, 3] = 1.0 / 9
     with pytest.raises(ValueError):
         programs.replace_program(m).blob()
+
+
+def test_group_batch_rejects_member_size_mismatch(tok):
+    """a member built for a different prompt count than the group size (its program,
+    alpha rows and LocalBlend slices are sized by it) is refused at construction."""
+    import pytest
+    from p2p_amd import controllers as pc
+    four = ["a cat eating a burger", "a dog eating a burger", "a cow eating a burger", "a cat eating a pizza"]
+    a = pc.AttentionReplace(four, 10, .8, .4, tokenizer=tok, device="cpu")
+    b = pc.AttentionReplace(four[:3], 10, .8, .4, tokenizer=tok, device="cpu")
+    with pytest.raises(ValueError):
+        pc.GroupBatch([a, b])
+    with pytest.raises(ValueError):
+        pc.GroupBatch([a], group_size=3)
+    c = pc.AttentionReplace(four, 10, .8, .4, tokenizer=tok, device="cpu")
+    c.store_self_maps = False
+    with pytest.raises(ValueError):
+        pc.GroupBatch([a, c])
+    assert pc.GroupBatch([a, pc.AttentionReplace(four, 10, .8, .4, tokenizer=tok, device="cpu")]).group_size == 4
+
+
+def test_aggregate_attention_needs_prompt_count_for_plain_store():
+    import pytest
+    import torch
+    from p2p_amd import controllers as pc
+    store = pc.AttentionStore()
+    store.attention_store = {"down_cross": [torch.rand(16, 256, 77)], "up_cross": [], "mid_cross": []}
+    store.cur_step = 2
+    with pytest.raises(ValueError, match="prompts="):
+        pc.aggregate_attention(store, 16, ["down"], True, 0)
+    out = pc.aggregate_attention(store, 16, ["down"], True, 1, prompts=["a", "b"])
+    assert out.shape == (16, 16, 77)
+    red = pc.reduce_maps(store, 16, ["down"], True, 2)
+    assert torch.allclose(red[1], out, atol=1e-6)
