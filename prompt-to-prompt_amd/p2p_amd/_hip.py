@@ -12,6 +12,10 @@ from typing import Optional, Sequence
 import torch
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libp2p_hip.so")
+# A/B timing tools load the experiments build (make EXPERIMENTS=1 OUTDIR=../p2p_amd/exp) instead;
+# it is built from the same sources (check_source_hash holds for it too)
+if os.environ.get("P2P_EXPERIMENTS_LIB") == "1":
+    _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "exp", "libp2p_hip.so")
 _lib = None
 
 # Optional launch observer (bench.py times the dominant kernel with HIP events through it):

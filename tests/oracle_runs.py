@@ -48,7 +48,7 @@ def oracle_group(model, prompts, x_T, ctrl, steps=50, guidance=7.5):
         for t in sched.timesteps:
             eps = model.unet(torch.cat([lat] * 2).to(udt), t, encoder_hidden_states=ctx)["sample"].float()
             eu, ec = eps.chunk(2)
-            lat = oc.ddim_prev(ac, ac[0], eu + guidance * (ec - eu), int(t), lat)
+            lat = oc.ddim_prev(ac, ac[0], eu + guidance * (ec - eu), int(t), lat, n_inf=steps)
             lat = ctrl.step_callback(lat)
     return lat
 

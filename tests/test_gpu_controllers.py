@@ -49,7 +49,10 @@ def run_pair(prod, orc, layers, steps, tol_out, tol_store, x_t=None, seed=0, qsc
             probs = orc(probs, is_cross, place)
             want = ref_out(probs.reshape(N, H, P, K), v, H)
             err = (out - want).abs().max().item()
-            assert err < tol_out, (step, place, is_cross, P, err)
+            # the bf16 PV bound scales with the row mass of the (edited) probabilities: a reweight
+            # row sums to up to max(eq), not 1 (|dO| <= 2^-7 * sum_k |p'_k| * max|V|)
+            mass = max(1.0, probs.abs().sum(-1).max().item())
+            assert err < tol_out * mass, (step, place, is_cross, P, err, mass)
         if x_t is not None:
             a = prod.step_callback(x_t)
             b = orc.step_callback(x_t)

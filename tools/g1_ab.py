@@ -1,0 +1,85 @@
+"""A/B of the G1/G7 self-attention kernel schedules (one variant per process: the experiments
+build reads P2P_SELF_VARIANT once at load).  Checks the variant against a torch fp32 reference on
+the same bf16 inputs (plain, peaky rows, a source-map remap, ragged P/K), then times the config-2
+G1 launch (N = 8, H = 8, P = K = 4096, d = 40) with HIP events: median of 7 rounds x 50 launches.
+Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=v python tools/g1_ab.py"""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prompt-to-prompt_amd"))
+import torch  # noqa: E402
+
+from p2p_amd import _hip  # noqa: E402
+
+
+def ref(q, k, v, H, qk_src=None):
+    N, P, C = q.shape
+    d = C // H
+    qs = q if qk_src is None else q[qk_src]
+    ks = k if qk_src is None else k[qk_src]
+    qh = qs.float().reshape(N, P, H, d).permute(0, 2, 1, 3)
+    kh = ks.float().reshape(N, -1, H, d).permute(0, 2, 1, 3)
+    vh = v.float().reshape(N, -1, H, d).permute(0, 2, 1, 3)
+    p = (qh @ kh.transpose(-1, -2) * d ** -0.5).softmax(-1)
+    return (p @ vh).permute(0, 2, 1, 3).reshape(N, P, C)
+
+
+def check(N, P, K, d, H=8, qscale=1.0, qk_src=None, dtype=torch.bfloat16):
+    g = torch.Generator(device="cuda").manual_seed(P * 7 + K)
+    C = H * d
+    q = (qscale * torch.randn(N, P, C, device="cuda", generator=g)).to(dtype)
+    k = torch.randn(N, K, C, device="cuda", generator=g).to(dtype)
+    v = torch.randn(N, K, C, device="cuda", generator=g).to(dtype)
+    o = torch.empty_like(q)
+    _hip.self_attn(q, k, v, o, H, d ** -0.5, qk_src=qk_src)
+    want = ref(q, k, v, H, qk_src)
+    return (o.float() - want).abs().max().item() / v.float().abs().max().item()
+
+
+def time_fn(fn, iters=50, warm=3):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    var = int(os.environ.get("P2P_SELF_VARIANT", "0"))
+    errs = {
+        "g1": check(8, 4096, 4096, 40),
+        "peaky16": check(2, 4096, 4096, 40, qscale=16.0),
+        "remap": check(8, 1024, 1024, 40, qk_src=[0, 1, 2, 3, 4, 4, 4, 4]),
+        "ragged": check(2, 1000, 777, 40),
+        "f32in": check(2, 2048, 2048, 40, dtype=torch.float32),
+    }
+    ok = all(e < 2.0 ** -7 * 2 for e in errs.values())
+    N, H, P, d = 8, 8, 4096, 40
+    C = H * d
+    q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    k = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    v = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    o = torch.empty_like(q)
+    fn = lambda: _hip.self_attn(q, k, v, o, H, d ** -0.5)  # noqa: E731
+    t_end = time.time() + 1.0
+    while time.time() < t_end:
+        fn()
+    torch.cuda.synchronize()
+    rounds = [time_fn(fn) for _ in range(7)]
+    ms = statistics.median(rounds)
+    flop = 4.0 * P * P * C * N
+    print(json.dumps({"variant": var, "ok": ok, "rel_err": {k_: round(e, 5) for k_, e in errs.items()},
+                      "median_ms": round(ms, 4), "min_ms": round(min(rounds), 4),
+                      "tflops": round(flop / ms / 1e9, 1), "frac_2p5": round(flop / ms / 1e9 / 2500, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
