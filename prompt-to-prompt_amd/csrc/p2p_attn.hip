@@ -162,7 +162,16 @@ __global__ __launch_bounds__(64 * WAVES) void self_pv_kernel(SelfArgs a) {
 //  * EXACT (launches that keep maps): the row sum is the f32 sum of the exponentials (VALU adds),
 //    not the MFMA sum of their bf16 roundings, so the lse that self_maps_kernel normalises the
 //    stored maps with is f32-exact (a peaky row's bf16 rounding would otherwise be ~2e-3).
-template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, bool EXACT = false>
+//  * NOMAX (launches that want O only): no per-tile row max at all.  The first tile sets the
+//    reference point from its exact max; later tiles exponentiate against it directly and the
+//    row sum that the PV MFMA leaves in the ones column is checked once per tile: a row whose sum
+//    passes 2^64 is rescaled by 2^-64 (its reference moves up by 64).  bf16 P has the f32
+//    exponent range, so p may grow far past 1 without any loss of relative precision; only a
+//    logit jumping more than ~115 (log2 units) above the running reference within one tile could
+//    overflow -- that shows as a non-finite row sum, and then the whole workgroup recomputes
+//    its tiles with the max-tracking loop.  Saves the 8 v_max3 + reduction + decision of every
+//    32 x 32 block (the kernel is VALU-issue-bound at d = 40).
+template <typename IO, typename MQ, typename MP, int D, int BK, int WAVES, bool EXACT = false, bool NOMAX = false>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -293,7 +302,8 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
   __syncthreads();
   // one K/V tile; the key mask exists only in the instantiation for a partial last tile (as a
   // runtime branch the compiler if-converted it: ~100 extra VALU per tile on every tile)
-  auto tile = [&](int kt, auto masked) {
+  bool bad = false;  // NOMAX: some row sum of this lane went non-finite
+  auto tile = [&](int kt, auto masked, auto fast) {
     const int buf = kt & 1;
     if (kt + 1 < ntiles) stage_load(kt + 1);
     float sv[NSB][16];
@@ -316,22 +326,24 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
         for (int r = 0; r < 16; ++r)
           if (kt * BK + sb * 32 + acc_row(r, hh) >= K) sv[sb][r] = -INFINITY;
     }
-    float mx = -INFINITY;
+    if constexpr (!decltype(fast)::value) {
+      float mx = -INFINITY;
 #pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
+      for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
-    mx = fmaxf(mx, other_half(mx)) * c;
-    // defer-max: move the reference point only when this tile overshoots it by > thr
-    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
-      const float mnew = fmaxf(m_run, mx);
-      const float alpha = fast_exp2(m_run - mnew);
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[sb][r]);
+      mx = fmaxf(mx, other_half(mx)) * c;
+      // defer-max: move the reference point only when this tile overshoots it by > thr
+      if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
+        const float mnew = fmaxf(m_run, mx);
+        const float alpha = fast_exp2(m_run - mnew);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
+        for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
-      l_run *= alpha;
-      m_run = mnew;
+          for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+        l_run *= alpha;
+        m_run = mnew;
+      }
     }
     float ls = 0.f;
 #pragma unroll
@@ -346,12 +358,53 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
     const EV* Vb = Vs + buf * VBUF;
 #pragma unroll
     for (int sb = 0; sb < NSB; ++sb) pv_block<VS, NDT>(MP{}, O, Vb, sb * 32, sv[sb], lane);
+    if constexpr (decltype(fast)::value) {
+      // the row sum so far (ones column; lanes kLh of the pair hold it, the other half a zero
+      // pad column): rescale rows past 2^64, flag non-finite ones
+      const float own = O[kLdt][kLr];
+      const float lsum = own + other_half(own);
+      bad |= !(lsum < INFINITY);
+      if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
+        if (lsum > 0x1p64f) {
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) O[dt][r] *= 0x1p-64f;
+          m_run += 64.f;
+        }
+      }
+    }
     if (kt + 1 < ntiles) stage_write(buf ^ 1);
     __syncthreads();
   };
   const int nfull = K / BK;
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
+  if constexpr (NOMAX) {
+    static_assert(kOnes, "NOMAX reads the row sum from the ones column");
+    __shared__ int wg_bad;
+    if (tid == 0) wg_bad = 0;
+    // tile 0 sets every row's reference point from its exact max
+    if (nfull == 0) tile(0, std::true_type{}, std::false_type{});
+    else tile(0, std::false_type{}, std::false_type{});
+    for (int kt = 1; kt < nfull; ++kt) tile(kt, std::false_type{}, std::true_type{});
+    if (nfull < ntiles && nfull > 0) tile(nfull, std::true_type{}, std::true_type{});
+    if (__any(bad) && lane == 0) wg_bad = 1;
+    __syncthreads();
+    if (__builtin_expect(wg_bad != 0, 0)) {
+      // some row overflowed: the whole workgroup recomputes with the max-tracking loop
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+      m_run = -INFINITY;
+      stage_load(0);
+      stage_write(0);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
+      for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{}, std::false_type{});
+      if (nfull < ntiles) tile(nfull, std::true_type{}, std::false_type{});
+    }
+  } else {
+    for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{}, std::false_type{});
+    if (nfull < ntiles) tile(nfull, std::true_type{}, std::false_type{});
+  }
   float l;
   if constexpr (kOnes) l = __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
   else l = l_run + __shfl_xor(l_run, 32);
@@ -369,6 +422,337 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
       }
     // row log-sum-exp for the backward pass (log2 domain, scale folded: p = exp2(c s - lse))
     if (a.lse && hh == 0) a.lse[(int64_t)(n * a.H + h) * a.P + p] = m_run + __log2f(l);
+  }
+}
+
+// ====================================================================== fused self attention, QB rows/wave
+// The NOMAX kernel above with QB 32-row query blocks per wave (the 4-wave structure of the CDNA4
+// attention playbook: one workgroup of WAVES waves still covers 32 * QB * WAVES queries).  Every
+// K fragment and V fragment read from LDS feeds QB MFMAs, and the QB blocks are independent
+// instruction streams inside the wave, so one block's exponentials can issue beside another
+// block's MFMAs without relying on the co-resident waves; with WAVES = 4 the waves sharing a SIMD
+// belong to different workgroups, so no barrier locks them into the same phase.
+template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool STREAM = false, int SCHED = 0>
+__global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a) {
+  using EK = typename MQ::elem;
+  using MP = MmaBf16;
+  constexpr int DK = (D + 15) / 16 * 16;
+  constexpr int DV = (D + 31) / 32 * 32;
+  static_assert(DV > D, "needs the ones column");
+  constexpr int NKT = DK / 16;
+  constexpr int NDT = DV / 32;
+  constexpr int NSB = BK / 32;
+  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
+  constexpr int VS = VStrideBf16<DV>::value;
+  constexpr int NT = 64 * WAVES;
+  constexpr int CPR = D / 8;
+  constexpr int NCH = (BK * CPR + NT - 1) / NT;
+  constexpr int KPLANE = BK * KS;
+  constexpr int KBUF = KPLANE * MQ::planes;
+  constexpr int VBUF = BK * VS;
+  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
+  constexpr int VBYTES = 2 * VBUF * 2;
+  constexpr int kLdt = D / 32;
+  constexpr int kLrr = D % 32;
+  constexpr int kLh = (kLrr >> 2) & 1;
+  constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+  constexpr float kRescaleThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
+  __shared__ int wg_bad;
+  EK* const Ks = reinterpret_cast<EK*>(smem);
+  uint16_t* const Vs = reinterpret_cast<uint16_t*>(smem + KBYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qi = lane & 31;
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H;
+  const int n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int pw = (qt * WAVES + wave) * 32 * QB;   // first query of this wave
+  const int K = a.K;
+  const float c = a.scale_log2;
+
+  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
+
+  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
+  if (tid == 0) wg_bad = 0;
+  __syncthreads();
+  for (int r = tid; r < 2 * BK; r += NT) Vs[r * VS + D] = 0x3F80;
+
+  typename MQ::frag qf[QB][NKT];
+#pragma unroll
+  for (int b = 0; b < QB; ++b)
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const int col = 16 * t + 8 * hh;
+      const int p = pw + 32 * b + qi;
+      qf[b][t] = (p < a.P && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+    }
+
+  Chunk8<IO> kreg[NCH], vreg[NCH];
+  uint32_t koff[NCH], voff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int cidx = tid + i * NT;
+    const int row = min(cidx / CPR, BK - 1);
+    const int ch = cidx - (cidx / CPR) * CPR;
+    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * (int)sizeof(IO));
+    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * (int)sizeof(IO));
+  }
+  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + D) * (int64_t)sizeof(IO);
+  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
+  const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
+  const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
+  auto stage_load = [&](int kt) {
+    const __amdgpu_buffer_rsrc_t rk =
+        make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
+    const __amdgpu_buffer_rsrc_t rv =
+        make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      if ((BK * CPR) % NT == 0 || tid + i * NT < BK * CPR) {
+        kreg[i].load_buf(rk, koff[i]);
+        vreg[i].load_buf(rv, voff[i]);
+      }
+    }
+  };
+  auto stage_write = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
+        vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
+      }
+    }
+  };
+
+  const int ntiles = (K + BK - 1) / BK;
+  f32x16_t O[QB][NDT];
+  float m_run[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    m_run[b] = -INFINITY;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) O[b][dt] = f32x16_t{};
+  }
+
+  stage_load(0);
+  stage_write(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  bool bad = false;
+  // One tile, sub-block by sub-block (Q K^T, [max decision], exp, P V): only one sub-block's scores
+  // per query block are live.  Slow tiles (the first one, and the overflow recompute) move the
+  // reference point per 32-key sub-block with the defer-max rule; fast tiles (NOMAX) do not.
+  auto overflow_check = [&]() {
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      const float own = O[b][kLdt][kLr];
+      const float lsum = own + other_half(own);
+      bad |= !(lsum < INFINITY);
+      if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
+        if (lsum > 0x1p64f) {
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) O[b][dt][r] *= 0x1p-64f;
+          m_run[b] += 64.f;
+        }
+      }
+    }
+  };
+  // Whole-tile fast body (no max): all Q K^T, all exponentials, all P V; with SCHED the MFMAs
+  // and the VALU work are interleaved explicitly (sched_group_barrier): the second sub-block's
+  // Q K^T beside the first's exponentials, each P V beside the next exponentials / packs.
+  auto tile_whole = [&](int kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_load(kt + 1);
+    const EK* Kb = Ks + buf * KBUF;
+    const uint16_t* Vb = Vs + buf * VBUF;
+    float sv[QB][NSB][16];
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      f32x16_t acc[QB];
+#pragma unroll
+      for (int b = 0; b < QB; ++b) acc[b] = f32x16_t{};
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) MQ::mma(acc[b], fa, qf[b][t]);
+      }
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[b][sb][r] = fast_exp2(fmaf(acc[b][r], c, -m_run[b]));
+    }
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        MmaBf16::frag pb[QB];
+#pragma unroll
+        for (int b = 0; b < QB; ++b) pb[b] = MmaBf16::pack_p(sv[b][sb] + 8 * s2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const MmaBf16::frag af = vt_frag<VS>(Vb, sb * 32, s2, dt * 32, lane);
+#pragma unroll
+          for (int b = 0; b < QB; ++b) MmaBf16::mma(O[b][dt], af, pb[b]);
+        }
+      }
+    if constexpr (SCHED > 0 && NSB == 2 && QB == 2) {
+      // 6 QK(sb0) MFMAs with the K reads; 6 QK(sb1) MFMAs x 10 VALU (exp sb0);
+      // 16 PV MFMAs x 7 VALU (exp sb1, packs) with the V reads two at a time
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, SCHED == 1 ? 10 : 8, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, SCHED == 1 ? 7 : 8, 0);
+      }
+    }
+    overflow_check();
+    if (kt + 1 < ntiles) stage_write(buf ^ 1);
+    __syncthreads();
+  };
+  auto tile = [&](int kt, auto masked, auto fast) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_load(kt + 1);
+    const EK* Kb = Ks + buf * KBUF;
+    const uint16_t* Vb = Vs + buf * VBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      f32x16_t acc[QB];
+#pragma unroll
+      for (int b = 0; b < QB; ++b) acc[b] = f32x16_t{};
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) MQ::mma(acc[b], fa, qf[b][t]);
+      }
+      float sv[QB][16];
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sv[b][r] = acc[b][r];
+          if constexpr (decltype(masked)::value)
+            if (kt * BK + sb * 32 + acc_row(r, hh) >= K) sv[b][r] = -INFINITY;
+        }
+      if constexpr (!decltype(fast)::value) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[b][r]);
+          mx = fmaxf(mx, other_half(mx)) * c;
+          if (__builtin_expect(!__all(mx <= m_run[b] + kRescaleThr), 0)) {
+            const float mnew = fmaxf(m_run[b], mx);
+            const float alpha = fast_exp2(m_run[b] - mnew);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) O[b][dt][r] *= alpha;
+            m_run[b] = mnew;
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[b][r] = fast_exp2(fmaf(sv[b][r], c, -m_run[b]));
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        MmaBf16::frag pb[QB];
+#pragma unroll
+        for (int b = 0; b < QB; ++b) pb[b] = MmaBf16::pack_p(sv[b] + 8 * s2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const MmaBf16::frag af = vt_frag<VS>(Vb, sb * 32, s2, dt * 32, lane);
+#pragma unroll
+          for (int b = 0; b < QB; ++b) MmaBf16::mma(O[b][dt], af, pb[b]);
+        }
+      }
+    }
+    if constexpr (decltype(fast)::value) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        const float own = O[b][kLdt][kLr];
+        const float lsum = own + other_half(own);
+        bad |= !(lsum < INFINITY);
+        if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
+          if (lsum > 0x1p64f) {
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) O[b][dt][r] *= 0x1p-64f;
+            m_run[b] += 64.f;
+          }
+        }
+      }
+    }
+    if (kt + 1 < ntiles) stage_write(buf ^ 1);
+    __syncthreads();
+  };
+  const int nfull = K / BK;
+  if (nfull == 0) tile(0, std::true_type{}, std::false_type{});
+  else tile(0, std::false_type{}, std::false_type{});
+  for (int kt = 1; kt < nfull; ++kt) {
+    if constexpr (STREAM) tile(kt, std::false_type{}, std::true_type{});
+    else tile_whole(kt);
+  }
+  if (nfull < ntiles && nfull > 0) tile(nfull, std::true_type{}, std::true_type{});
+  if (__any(bad) && lane == 0) wg_bad = 1;
+  __syncthreads();
+  if (__builtin_expect(wg_bad != 0, 0)) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      m_run[b] = -INFINITY;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) O[b][dt] = f32x16_t{};
+    }
+    stage_load(0);
+    stage_write(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{}, std::false_type{});
+    if (nfull < ntiles) tile(nfull, std::true_type{}, std::false_type{});
+  }
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const float l = __shfl(O[b][kLdt][kLr], (lane & 31) + 32 * kLh);
+    const float inv = 1.f / l;
+    const int p = pw + 32 * b + qi;
+    if (p < a.P) {
+      IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = dt * 32 + 8 * g + 4 * hh;
+          if (dd < D)
+            store4(op + dd, O[b][dt][4 * g] * inv, O[b][dt][4 * g + 1] * inv, O[b][dt][4 * g + 2] * inv,
+                   O[b][dt][4 * g + 3] * inv);
+        }
+    }
   }
 }
 
@@ -608,6 +992,236 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused16_kernel(SelfArgs 
 
   // epilogue: row r of O[mt] is query p0w + 16 mt + 4 g + r; its sum sits in lane column D % 16
   // of tile D / 16 of the same 16-lane group
+  IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
+  const int dcol = lane & 15;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float l = __shfl(O[mt][kLnt][r], (lane & 48) | kLcol);
+      const float inv = 1.f / l;
+      const int q = p0w + 16 * mt + 4 * g16 + r;
+      if (q < a.P) {
+#pragma unroll
+        for (int nt = 0; nt < NNT; ++nt) {
+          const int d = nt * 16 + dcol;
+          if (d < D) {
+            const float v = O[mt][nt][r] * inv;
+            if constexpr (sizeof(IO) == 2) op[(int64_t)q * a.ldo + d] = f2bf(v);
+            else op[(int64_t)q * a.ldo + d] = v;
+          }
+        }
+      }
+    }
+}
+
+// ====================================================================== fused self attention, pipelined
+// self_attn_fused16_kernel with the two halves of consecutive tiles overlapped inside a wave:
+// iteration t issues Q K(t+1)^T (MFMA) beside the exponentials of tile t (VALU), then P(t) V(t)
+// (MFMA) beside the row max / rescale decision of tile t+1 (VALU).  K therefore runs one tile
+// ahead of V in the LDS rings: iteration t reads K(t+1) and V(t) and writes K(t+2) and V(t+1)
+// (two buffers each, one barrier per tile).  The lazy-rescale order stays safe (T13): the
+// decision for tile t+1 multiplies O only after P(t) V(t) has entered it, and P(t+1) is
+// exponentiated after that decision.  Needs K % BK == 0 (the launcher checks).
+template <typename IO, typename MQ, int D, int BK, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void self_attn_pipe_kernel(SelfArgs a) {
+  using EK = typename MQ::elem;
+  constexpr int DK = (D + 15) / 16 * 16;
+  constexpr int DV = (D + 1 + 15) / 16 * 16;
+  static_assert(DV <= 64, "the swizzled V image holds 64 columns");
+  constexpr int NKT = DK / 16;
+  constexpr int NNT = DV / 16;
+  constexpr int NSB = BK / 32;
+  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
+  constexpr int NT = 64 * WAVES;
+  constexpr int CPR = D / 8;
+  constexpr int NCH = (BK * CPR + NT - 1) / NT;
+  constexpr int KPLANE = BK * KS;
+  constexpr int KBUF = KPLANE * MQ::planes;
+  constexpr int VBUF = BK * 64;
+  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
+  constexpr int VBYTES = 2 * VBUF * 2;
+  constexpr int kLnt = D / 16, kLcol = D % 16;
+  constexpr float kRescaleThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
+  EK* const Ks = reinterpret_cast<EK*>(smem);
+  uint16_t* const Vs = reinterpret_cast<uint16_t*>(smem + KBYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qi = lane & 31;
+  const int g16 = lane >> 4;
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H;
+  const int n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int p0w = qt * 32 * WAVES + wave * 32;
+  const int p = p0w + qi;
+  const bool prow = p < a.P;
+  const int K = a.K;
+  const float c = a.scale_log2;
+
+  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
+
+  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
+  __syncthreads();
+  for (int r = tid; r < 2 * BK; r += NT) Vs[(r / BK) * VBUF + v16_off(r % BK, D)] = 0x3F80;
+
+  typename MQ::frag qf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int col = 16 * t + 8 * hh;
+    qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+  }
+
+  Chunk8<IO> kreg[NCH], vreg[NCH];
+  uint32_t koff[NCH], voff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int cidx = tid + i * NT;
+    const int row = min(cidx / CPR, BK - 1);
+    const int ch = cidx - (cidx / CPR) * CPR;
+    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * (int)sizeof(IO));
+    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * (int)sizeof(IO));
+  }
+  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + D) * (int64_t)sizeof(IO);
+  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
+  const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
+  const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
+  constexpr bool kAllThreads = (BK * CPR) % NT == 0;
+  auto load_k = [&](int kt) {
+    const __amdgpu_buffer_rsrc_t rk =
+        make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (kAllThreads || tid + i * NT < BK * CPR) kreg[i].load_buf(rk, koff[i]);
+  };
+  auto load_v = [&](int kt) {
+    const __amdgpu_buffer_rsrc_t rv =
+        make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (kAllThreads || tid + i * NT < BK * CPR) vreg[i].load_buf(rv, voff[i]);
+  };
+  auto write_k = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      if (kAllThreads || cidx < BK * CPR) {
+        const int row = cidx / CPR;
+        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + (cidx - row * CPR) * 8, KPLANE);
+      }
+    }
+  };
+  auto write_v = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      if (kAllThreads || cidx < BK * CPR) {
+        const int row = cidx / CPR;
+        vreg[i].store(Vs + buf * VBUF + v16_off(row, (cidx - row * CPR) * 8));
+      }
+    }
+  };
+
+  const int ntiles = K / BK;
+  f32x4_t O[2][NNT];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NNT; ++nt) O[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY;
+
+  auto qk = [&](int kt, float (&sv)[NSB][16]) {
+    const EK* Kb = Ks + (kt & 1) * KBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      f32x16_t acc = {};
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+        MQ::mma(acc, fa, qf[t]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
+    }
+  };
+  auto decide = [&](const float (&sv)[NSB][16]) {
+    float m4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m4[j] = -INFINITY;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int j = (sb * 8 + r / 2) & 3;
+        m4[j] = fmaxf(fmaxf(m4[j], sv[sb][r]), sv[sb][r + 1]);
+      }
+    float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    mx = fmaxf(mx, other_half(mx)) * c;
+    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - mnew);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, 16 * mt + 4 * g16 + r);
+#pragma unroll
+          for (int nt = 0; nt < NNT; ++nt) O[mt][nt][r] *= ar;
+        }
+      m_run = mnew;
+    }
+  };
+  auto softmax_pv = [&](int kt, float (&sv)[NSB][16]) {
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[sb][r] = fast_exp2(fmaf(sv[sb][r], c, -m_run));
+    const uint16_t* Vb = Vs + (kt & 1) * VBUF;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) pv16_block<NNT>(O, Vb, sb * 32, sv[sb], lane);
+  };
+
+  // prologue: K0, V0 and K1 in LDS; S(0) and its rescale decision
+  load_k(0);
+  load_v(0);
+  write_k(0);
+  write_v(0);
+  if (ntiles > 1) {
+    load_k(1);
+    write_k(1);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  float sA[NSB][16], sB[NSB][16];
+  qk(0, sA);
+  decide(sA);
+  auto iter = [&](int t, float (&cur)[NSB][16], float (&nxt)[NSB][16]) {
+    const bool more = t + 1 < ntiles;
+    if (t + 2 < ntiles) load_k(t + 2);
+    if (more) load_v(t + 1);
+    if (more) qk(t + 1, nxt);      // MFMA ...
+    softmax_pv(t, cur);            // ... beside the exponentials, then P V
+    if (more) decide(nxt);         // row max of t+1 beside P V
+    if (t + 2 < ntiles) write_k(t & 1);
+    if (more) write_v((t + 1) & 1);
+    __syncthreads();
+  };
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    iter(t, sA, sB);
+    iter(t + 1, sB, sA);
+  }
+  if (t < ntiles) iter(t, sA, sB);
+
   IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
   const int dcol = lane & 15;
 #pragma unroll
@@ -1207,9 +1821,16 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  constexpr bool kOnes = ((D + 31) / 32 * 32) > D;
   if (a.n_maps > 0)  // the lse feeds stored maps: exact f32 row sums
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
-  else
+  else if constexpr (kOnes && MP::kElemBytes == 2) {
+    // O only (no lse): no per-tile max (P2P_SELF_VARIANT 16 in an experiments build keeps it)
+    if (a.lse == nullptr && a.variant != 16 && a.variant != 30)
+      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false, true>), grid, block, 0, st, b);
+    else
+      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+  } else
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
@@ -1221,16 +1842,62 @@ static void launch_fused16(const SelfArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((self_attn_fused16_kernel<IO, MQ, D, BK, W>), grid, block, 0, st, b);
 }
 
+template <typename IO, typename MQ, int D, int BK, int W, int QB, bool STREAM = false, int SCHED = 0>
+static void launch_multi(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, STREAM, SCHED>), grid, block, 0, st, b);
+}
+
+template <typename IO, typename MQ, int D, int BK, int W>
+static void launch_pipe(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_attn_pipe_kernel<IO, MQ, D, BK, W>), grid, block, 0, st, b);
+}
+
 template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
   if constexpr (MP::kElemBytes == 2 && D == 40) {
-    // d = 40 on the bf16 pipe, nothing but O wanted: 16x16 P V (P2P_SELF_VARIANT 8 / 9 in an
-    // experiments build: the 32x32 kernel / 4-wave workgroups, for A/B timing)
-    if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64 && a.variant != 8) {
-      if (a.variant == 9) launch_fused16<IO, MQ, D, 64, 4>(a, st);
-      else launch_fused16<IO, MQ, D, 64, 8>(a, st);
-      return hipGetLastError();
+    // d = 40 on the bf16 pipe, nothing but O wanted: the 16x16-PV kernels (experiments build,
+    // P2P_SELF_VARIANT 10 / 11: fused16 8 / 4 waves; 12 / 13 / 14: pipelined BK 32 x 8 waves,
+    // 64 x 4, 64 x 8)
+    if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
+      // production: two 32-row query blocks per wave, 128-key tiles, 8-wave workgroups (512
+      // queries each: only where that still gives >= 4 workgroups per CU row of the grid)
+      if (a.variant == 0 && a.P >= 2048) {
+        launch_multi<IO, MQ, D, 128, 8, 2, true>(a, st);
+        return hipGetLastError();
+      }
+      switch (a.variant) {
+        case 27:
+          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, true>(a, st); return hipGetLastError(); }
+          break;
+        case 28: launch_multi<IO, MQ, D, 128, 4, 2, true>(a, st); return hipGetLastError();
+        case 10: launch_fused16<IO, MQ, D, 64, 8>(a, st); return hipGetLastError();
+        case 11: launch_fused16<IO, MQ, D, 64, 4>(a, st); return hipGetLastError();
+        case 17: launch_multi<IO, MQ, D, 64, 4, 2>(a, st); return hipGetLastError();
+        case 18: launch_multi<IO, MQ, D, 64, 8, 2>(a, st); return hipGetLastError();
+        case 19: launch_multi<IO, MQ, D, 32, 4, 2>(a, st); return hipGetLastError();
+        case 20: launch_multi<IO, MQ, D, 64, 4, 1>(a, st); return hipGetLastError();
+        case 21: launch_multi<IO, MQ, D, 64, 8, 2, true>(a, st); return hipGetLastError();
+        case 22: launch_multi<IO, MQ, D, 64, 4, 2, true>(a, st); return hipGetLastError();
+        case 23: launch_multi<IO, MQ, D, 128, 8, 2, true>(a, st); return hipGetLastError();
+        case 24: launch_multi<IO, MQ, D, 64, 8, 2, false, 1>(a, st); return hipGetLastError();
+        case 25: launch_multi<IO, MQ, D, 64, 8, 2, false, 2>(a, st); return hipGetLastError();
+        case 26: launch_multi<IO, MQ, D, 64, 4, 2, false, 1>(a, st); return hipGetLastError();
+        default: break;
+      }
+      if (a.variant >= 12 && a.variant <= 15 && a.K % 64 == 0) {
+        if (a.variant == 12) launch_pipe<IO, MQ, D, 32, 8>(a, st);
+        else if (a.variant == 13) launch_pipe<IO, MQ, D, 64, 4>(a, st);
+        else if (a.variant == 14) launch_pipe<IO, MQ, D, 64, 8>(a, st);
+        else launch_pipe<IO, MQ, D, 32, 4>(a, st);
+        return hipGetLastError();
+      }
     }
   }
   if (mode == MODE_FUSED) {
