@@ -426,16 +426,18 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 }
 
 // ====================================================================== fused self attention, QB rows/wave
-// The NOMAX kernel above with QB 32-row query blocks per wave (the 4-wave structure of the CDNA4
-// attention playbook: one workgroup of WAVES waves still covers 32 * QB * WAVES queries).  Every
-// K fragment and V fragment read from LDS feeds QB MFMAs, and the QB blocks are independent
-// instruction streams inside the wave, so one block's exponentials can issue beside another
-// block's MFMAs without relying on the co-resident waves; with WAVES = 4 the waves sharing a SIMD
-// belong to different workgroups, so no barrier locks them into the same phase.
-template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool STREAM = false, int SCHED = 0>
+// The production d = 40 kernel (G1/G7 without kept maps or autograd): the NOMAX loop above with
+// QB 32-row query blocks per wave.  Every K fragment and V fragment read from LDS feeds QB MFMAs
+// (half the LDS reads per FLOP at QB = 2), the QB blocks are independent instruction streams in
+// the wave, and a tile runs sub-block by sub-block (Q K^T, [max decision], exp, P V) so only one
+// 32-key sub-block of scores per block is live; 128-key tiles halve the barriers.  Slow tiles
+// (the first one, and the overflow recompute) move the reference point per sub-block with the
+// defer-max rule -- the sub-block's P V follows at once, so no P is pending at a rescale.
+// Measured at G1 (N = 8, H = 8, bf16; tools/g1_ab.py, profiles/r02): 0.239 ms (64-key tiles with
+// the per-tile max, one block per wave) -> 0.233 (NOMAX) -> 0.217 (this, QB = 2, BK = 128).
+template <typename IO, typename MQ, int D, int BK, int WAVES, int QB>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
-  using MP = MmaBf16;
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   static_assert(DV > D, "needs the ones column");
@@ -555,83 +557,6 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   // One tile, sub-block by sub-block (Q K^T, [max decision], exp, P V): only one sub-block's scores
   // per query block are live.  Slow tiles (the first one, and the overflow recompute) move the
   // reference point per 32-key sub-block with the defer-max rule; fast tiles (NOMAX) do not.
-  auto overflow_check = [&]() {
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      const float own = O[b][kLdt][kLr];
-      const float lsum = own + other_half(own);
-      bad |= !(lsum < INFINITY);
-      if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
-        if (lsum > 0x1p64f) {
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) O[b][dt][r] *= 0x1p-64f;
-          m_run[b] += 64.f;
-        }
-      }
-    }
-  };
-  // Whole-tile fast body (no max): all Q K^T, all exponentials, all P V; with SCHED the MFMAs
-  // and the VALU work are interleaved explicitly (sched_group_barrier): the second sub-block's
-  // Q K^T beside the first's exponentials, each P V beside the next exponentials / packs.
-  auto tile_whole = [&](int kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < ntiles) stage_load(kt + 1);
-    const EK* Kb = Ks + buf * KBUF;
-    const uint16_t* Vb = Vs + buf * VBUF;
-    float sv[QB][NSB][16];
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      f32x16_t acc[QB];
-#pragma unroll
-      for (int b = 0; b < QB; ++b) acc[b] = f32x16_t{};
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
-#pragma unroll
-        for (int b = 0; b < QB; ++b) MQ::mma(acc[b], fa, qf[b][t]);
-      }
-#pragma unroll
-      for (int b = 0; b < QB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sv[b][sb][r] = fast_exp2(fmaf(acc[b][r], c, -m_run[b]));
-    }
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        MmaBf16::frag pb[QB];
-#pragma unroll
-        for (int b = 0; b < QB; ++b) pb[b] = MmaBf16::pack_p(sv[b][sb] + 8 * s2);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const MmaBf16::frag af = vt_frag<VS>(Vb, sb * 32, s2, dt * 32, lane);
-#pragma unroll
-          for (int b = 0; b < QB; ++b) MmaBf16::mma(O[b][dt], af, pb[b]);
-        }
-      }
-    if constexpr (SCHED > 0 && NSB == 2 && QB == 2) {
-      // 6 QK(sb0) MFMAs with the K reads; 6 QK(sb1) MFMAs x 10 VALU (exp sb0);
-      // 16 PV MFMAs x 7 VALU (exp sb1, packs) with the V reads two at a time
-      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, SCHED == 1 ? 10 : 8, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, SCHED == 1 ? 7 : 8, 0);
-      }
-    }
-    overflow_check();
-    if (kt + 1 < ntiles) stage_write(buf ^ 1);
-    __syncthreads();
-  };
   auto tile = [&](int kt, auto masked, auto fast) {
     const int buf = kt & 1;
     if (kt + 1 < ntiles) stage_load(kt + 1);
@@ -715,10 +640,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   const int nfull = K / BK;
   if (nfull == 0) tile(0, std::true_type{}, std::false_type{});
   else tile(0, std::false_type{}, std::false_type{});
-  for (int kt = 1; kt < nfull; ++kt) {
-    if constexpr (STREAM) tile(kt, std::false_type{}, std::true_type{});
-    else tile_whole(kt);
-  }
+  for (int kt = 1; kt < nfull; ++kt) tile(kt, std::false_type{}, std::true_type{});
   if (nfull < ntiles && nfull > 0) tile(nfull, std::true_type{}, std::true_type{});
   if (__any(bad) && lane == 0) wg_bad = 1;
   __syncthreads();
@@ -754,495 +676,6 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
         }
     }
   }
-}
-
-// ====================================================================== fused self attention, 16x16 PV
-// The d = 40 hot kernel (G1/G7) with P V on v_mfma_f32_16x16x32_bf16.  Q K^T stays on the 32x32x16
-// MFMA in the S^T orientation (query on the lane, one lane pair per softmax row, as above); P V
-// is computed NON-transposed, O = P V, with d on the 16-wide N side, so d = 40 plus the row-sum
-// column pads to 48 instead of 64 (the 32x32 PV of self_attn_fused_kernel issues 64 columns):
-// per 32 x 32 block 3 + 6 MFMAs = 96 + 96 cycles instead of 96 + 128.
-// The A operand (P, 16 queries x 32 keys) needs query = lane & 15 in all four lane groups, while
-// the S^T accumulator holds query = lane & 31: after the bf16 packing, one v_permlane16_swap per
-// pair of packed dwords (4 per block) moves the 16-lane rows of queries 0-15 / 16-31 together --
-// no LDS round trip.  Pairing dwords (0,2) (1,3) (4,6) (5,7) gives lane group g the keys
-// {0, 8, 4, 12}[g] + 0..3 and + 16..19 of the block (k order is free as long as V matches), and
-// the V fragments are two ds_read_b64_tr_b16 per 16-column d tile from a row-major [keys][64]
-// image whose 16-byte chunks are XOR-swizzled by bits 1 and 3 of the row: the two 4-row blocks a
-// half-wave reads (8 rows apart) then hit all 64 banks once.
-// O (16x16 accumulators) keeps the query on the accumulator row, so the (rare) lazy rescale and
-// the final 1/l fetch their per-query factor with a lane shuffle.  Production path for launches
-// that keep no maps and return no lse (the EXACT / autograd instantiations stay on the kernel
-// above).
-__device__ __forceinline__ int v16_off(int row, int col) {
-  const int t = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-  return row * 64 + ((((col >> 3) ^ (t << 1))) << 3) + (col & 7);
-}
-
-template <int NNT>
-__device__ __forceinline__ void pv16_block(f32x4_t (&O)[2][NNT], const uint16_t* V, int row0,
-                                           const float (&p)[16], int lane) {
-  typedef __attribute__((ext_vector_type(4))) float f4;
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-  uint32_t dw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)  // one v_cvt_pk_bf16_f32 per pair
-    dw[i] = __builtin_bit_cast(uint32_t, bf16x2_t{(__bf16)p[2 * i], (__bf16)p[2 * i + 1]});
-  uint32_t a0[4], a1[4];
-  {
-    const auto r0 = __builtin_amdgcn_permlane16_swap(dw[0], dw[2], false, false);
-    const auto r1 = __builtin_amdgcn_permlane16_swap(dw[1], dw[3], false, false);
-    const auto r2 = __builtin_amdgcn_permlane16_swap(dw[4], dw[6], false, false);
-    const auto r3 = __builtin_amdgcn_permlane16_swap(dw[5], dw[7], false, false);
-    a0[0] = r0[0]; a1[0] = r0[1];
-    a0[1] = r1[0]; a1[1] = r1[1];
-    a0[2] = r2[0]; a1[2] = r2[1];
-    a0[3] = r3[0]; a1[3] = r3[1];
-  }
-  const bf16x8_t A0 = __builtin_bit_cast(bf16x8_t, u32x4_t{a0[0], a0[1], a0[2], a0[3]});
-  const bf16x8_t A1 = __builtin_bit_cast(bf16x8_t, u32x4_t{a1[0], a1[1], a1[2], a1[3]});
-  const int g = lane >> 4, i = lane & 15;
-  const int r = row0 + ((g & 1) << 3) + ((g >> 1) << 2) + (i >> 2);
-  typedef __attribute__((address_space(3))) short4_t lds_s4;
-#pragma unroll
-  for (int nt = 0; nt < NNT; ++nt) {
-    const int c = nt * 16 + 4 * (i & 3);
-    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(V + v16_off(r, c)));
-    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(V + v16_off(r + 16, c)));
-    const bf16x8_t B = __builtin_bit_cast(bf16x8_t, short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-    O[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B, O[0][nt], 0, 0, 0);
-    O[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B, O[1][nt], 0, 0, 0);
-  }
-}
-
-template <typename IO, typename MQ, int D, int BK, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void self_attn_fused16_kernel(SelfArgs a) {
-  using EK = typename MQ::elem;
-  constexpr int DK = (D + 15) / 16 * 16;
-  constexpr int DV = (D + 1 + 15) / 16 * 16;   // d plus the row-sum column, in 16-wide tiles
-  static_assert(DV <= 64, "the swizzled V image holds 64 columns");
-  constexpr int NKT = DK / 16;
-  constexpr int NNT = DV / 16;
-  constexpr int NSB = BK / 32;
-  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
-  constexpr int NT = 64 * WAVES;
-  constexpr int CPR = D / 8;
-  constexpr int NCH = (BK * CPR + NT - 1) / NT;
-  constexpr int KPLANE = BK * KS;
-  constexpr int KBUF = KPLANE * MQ::planes;
-  constexpr int VBUF = BK * 64;
-  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
-  constexpr int VBYTES = 2 * VBUF * 2;
-  constexpr int kLnt = D / 16, kLcol = D % 16;   // O tile / lane column of the row-sum column
-  constexpr float kRescaleThr = 8.0f;
-  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
-  EK* const Ks = reinterpret_cast<EK*>(smem);
-  uint16_t* const Vs = reinterpret_cast<uint16_t*>(smem + KBYTES);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int hh = lane >> 5;
-  const int qi = lane & 31;
-  const int g16 = lane >> 4;
-
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int qt = logical % a.n_qtiles;
-  const int nh = logical / a.n_qtiles;
-  const int h = nh % a.H;
-  const int n = nh / a.H;
-  const int src = a.qk_src[n];
-  const int p0w = qt * 32 * WAVES + wave * 32;
-  const int p = p0w + qi;
-  const bool prow = p < a.P;
-  const int K = a.K;
-  const float c = a.scale_log2;
-
-  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
-  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
-  const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
-
-  // LDS image: zero pads; V column D = 1 in every row of both buffers (the row-sum column)
-  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
-  __syncthreads();
-  for (int r = tid; r < 2 * BK; r += NT) Vs[(r / BK) * VBUF + v16_off(r % BK, D)] = 0x3F80;
-
-  typename MQ::frag qf[NKT];
-#pragma unroll
-  for (int t = 0; t < NKT; ++t) {
-    const int col = 16 * t + 8 * hh;
-    qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
-  }
-
-  Chunk8<IO> kreg[NCH], vreg[NCH];
-  uint32_t koff[NCH], voff[NCH];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int cidx = tid + i * NT;
-    const int row = min(cidx / CPR, BK - 1);
-    const int ch = cidx - (cidx / CPR) * CPR;
-    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * (int)sizeof(IO));
-    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * (int)sizeof(IO));
-  }
-  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + D) * (int64_t)sizeof(IO);
-  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
-  const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
-  const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
-  auto stage_load = [&](int kt) {
-    const __amdgpu_buffer_rsrc_t rk =
-        make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
-    const __amdgpu_buffer_rsrc_t rv =
-        make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int cidx = tid + i * NT;
-      if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
-        kreg[i].load_buf(rk, koff[i]);
-        vreg[i].load_buf(rv, voff[i]);
-      }
-    }
-  };
-  auto stage_write = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int cidx = tid + i * NT;
-      if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
-        const int row = cidx / CPR;
-        const int ch = cidx - row * CPR;
-        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
-        vreg[i].store(Vs + buf * VBUF + v16_off(row, ch * 8));
-      }
-    }
-  };
-
-  const int ntiles = (K + BK - 1) / BK;
-  f32x4_t O[2][NNT];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NNT; ++nt) O[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY;
-
-  stage_load(0);
-  stage_write(0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see self_attn_fused_kernel
-  __syncthreads();
-  auto tile = [&](int kt, auto masked) {
-    const int buf = kt & 1;
-    if (kt + 1 < ntiles) stage_load(kt + 1);
-    float sv[NSB][16];
-    const EK* Kb = Ks + buf * KBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      f32x16_t acc = {};
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
-        MQ::mma(acc, fa, qf[t]);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
-    }
-    if constexpr (decltype(masked)::value) {
-#pragma unroll
-      for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * BK + sb * 32 + acc_row(r, hh) >= K) sv[sb][r] = -INFINITY;
-    }
-    // row max as four independent max3 chains (latency), then combined
-    float m4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) m4[j] = -INFINITY;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {  // chain form: one v_max3 per pair, no canonicalising max
-        const int j = (sb * 8 + r / 2) & 3;
-        m4[j] = fmaxf(fmaxf(m4[j], sv[sb][r]), sv[sb][r + 1]);
-      }
-    float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    mx = fmaxf(mx, other_half(mx)) * c;
-    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
-      const float mnew = fmaxf(m_run, mx);
-      const float alpha = fast_exp2(m_run - mnew);
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ar = __shfl(alpha, 16 * mt + 4 * g16 + r);   // this accumulator row's query
-#pragma unroll
-          for (int nt = 0; nt < NNT; ++nt) O[mt][nt][r] *= ar;
-        }
-      m_run = mnew;
-    }
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sv[sb][r] = fast_exp2(fmaf(sv[sb][r], c, -m_run));
-    const uint16_t* Vb = Vs + buf * VBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) pv16_block<NNT>(O, Vb, sb * 32, sv[sb], lane);
-    if (kt + 1 < ntiles) stage_write(buf ^ 1);
-    __syncthreads();
-  };
-  const int nfull = K / BK;
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
-
-  // epilogue: row r of O[mt] is query p0w + 16 mt + 4 g + r; its sum sits in lane column D % 16
-  // of tile D / 16 of the same 16-lane group
-  IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
-  const int dcol = lane & 15;
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float l = __shfl(O[mt][kLnt][r], (lane & 48) | kLcol);
-      const float inv = 1.f / l;
-      const int q = p0w + 16 * mt + 4 * g16 + r;
-      if (q < a.P) {
-#pragma unroll
-        for (int nt = 0; nt < NNT; ++nt) {
-          const int d = nt * 16 + dcol;
-          if (d < D) {
-            const float v = O[mt][nt][r] * inv;
-            if constexpr (sizeof(IO) == 2) op[(int64_t)q * a.ldo + d] = f2bf(v);
-            else op[(int64_t)q * a.ldo + d] = v;
-          }
-        }
-      }
-    }
-}
-
-// ====================================================================== fused self attention, pipelined
-// self_attn_fused16_kernel with the two halves of consecutive tiles overlapped inside a wave:
-// iteration t issues Q K(t+1)^T (MFMA) beside the exponentials of tile t (VALU), then P(t) V(t)
-// (MFMA) beside the row max / rescale decision of tile t+1 (VALU).  K therefore runs one tile
-// ahead of V in the LDS rings: iteration t reads K(t+1) and V(t) and writes K(t+2) and V(t+1)
-// (two buffers each, one barrier per tile).  The lazy-rescale order stays safe (T13): the
-// decision for tile t+1 multiplies O only after P(t) V(t) has entered it, and P(t+1) is
-// exponentiated after that decision.  Needs K % BK == 0 (the launcher checks).
-template <typename IO, typename MQ, int D, int BK, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void self_attn_pipe_kernel(SelfArgs a) {
-  using EK = typename MQ::elem;
-  constexpr int DK = (D + 15) / 16 * 16;
-  constexpr int DV = (D + 1 + 15) / 16 * 16;
-  static_assert(DV <= 64, "the swizzled V image holds 64 columns");
-  constexpr int NKT = DK / 16;
-  constexpr int NNT = DV / 16;
-  constexpr int NSB = BK / 32;
-  constexpr int KS = KStride<DK, MQ::kElemBytes>::value;
-  constexpr int NT = 64 * WAVES;
-  constexpr int CPR = D / 8;
-  constexpr int NCH = (BK * CPR + NT - 1) / NT;
-  constexpr int KPLANE = BK * KS;
-  constexpr int KBUF = KPLANE * MQ::planes;
-  constexpr int VBUF = BK * 64;
-  constexpr int KBYTES = 2 * KBUF * (int)sizeof(EK);
-  constexpr int VBYTES = 2 * VBUF * 2;
-  constexpr int kLnt = D / 16, kLcol = D % 16;
-  constexpr float kRescaleThr = 8.0f;
-  __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
-  EK* const Ks = reinterpret_cast<EK*>(smem);
-  uint16_t* const Vs = reinterpret_cast<uint16_t*>(smem + KBYTES);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int hh = lane >> 5;
-  const int qi = lane & 31;
-  const int g16 = lane >> 4;
-
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int qt = logical % a.n_qtiles;
-  const int nh = logical / a.n_qtiles;
-  const int h = nh % a.H;
-  const int n = nh / a.H;
-  const int src = a.qk_src[n];
-  const int p0w = qt * 32 * WAVES + wave * 32;
-  const int p = p0w + qi;
-  const bool prow = p < a.P;
-  const int K = a.K;
-  const float c = a.scale_log2;
-
-  const IO* const qp = static_cast<const IO*>(a.q) + (int64_t)src * a.bsq + h * D;
-  const IO* const kp = static_cast<const IO*>(a.k) + (int64_t)src * a.bsk + h * D;
-  const IO* const vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
-
-  for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
-  __syncthreads();
-  for (int r = tid; r < 2 * BK; r += NT) Vs[(r / BK) * VBUF + v16_off(r % BK, D)] = 0x3F80;
-
-  typename MQ::frag qf[NKT];
-#pragma unroll
-  for (int t = 0; t < NKT; ++t) {
-    const int col = 16 * t + 8 * hh;
-    qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
-  }
-
-  Chunk8<IO> kreg[NCH], vreg[NCH];
-  uint32_t koff[NCH], voff[NCH];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int cidx = tid + i * NT;
-    const int row = min(cidx / CPR, BK - 1);
-    const int ch = cidx - (cidx / CPR) * CPR;
-    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * (int)sizeof(IO));
-    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * (int)sizeof(IO));
-  }
-  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + D) * (int64_t)sizeof(IO);
-  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
-  const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
-  const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
-  constexpr bool kAllThreads = (BK * CPR) % NT == 0;
-  auto load_k = [&](int kt) {
-    const __amdgpu_buffer_rsrc_t rk =
-        make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      if (kAllThreads || tid + i * NT < BK * CPR) kreg[i].load_buf(rk, koff[i]);
-  };
-  auto load_v = [&](int kt) {
-    const __amdgpu_buffer_rsrc_t rv =
-        make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      if (kAllThreads || tid + i * NT < BK * CPR) vreg[i].load_buf(rv, voff[i]);
-  };
-  auto write_k = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int cidx = tid + i * NT;
-      if (kAllThreads || cidx < BK * CPR) {
-        const int row = cidx / CPR;
-        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + (cidx - row * CPR) * 8, KPLANE);
-      }
-    }
-  };
-  auto write_v = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int cidx = tid + i * NT;
-      if (kAllThreads || cidx < BK * CPR) {
-        const int row = cidx / CPR;
-        vreg[i].store(Vs + buf * VBUF + v16_off(row, (cidx - row * CPR) * 8));
-      }
-    }
-  };
-
-  const int ntiles = K / BK;
-  f32x4_t O[2][NNT];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NNT; ++nt) O[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY;
-
-  auto qk = [&](int kt, float (&sv)[NSB][16]) {
-    const EK* Kb = Ks + (kt & 1) * KBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      f32x16_t acc = {};
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
-        MQ::mma(acc, fa, qf[t]);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sv[sb][r] = acc[r];
-    }
-  };
-  auto decide = [&](const float (&sv)[NSB][16]) {
-    float m4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) m4[j] = -INFINITY;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int j = (sb * 8 + r / 2) & 3;
-        m4[j] = fmaxf(fmaxf(m4[j], sv[sb][r]), sv[sb][r + 1]);
-      }
-    float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    mx = fmaxf(mx, other_half(mx)) * c;
-    if (__builtin_expect(!__all(mx <= m_run + kRescaleThr), 0)) {
-      const float mnew = fmaxf(m_run, mx);
-      const float alpha = fast_exp2(m_run - mnew);
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ar = __shfl(alpha, 16 * mt + 4 * g16 + r);
-#pragma unroll
-          for (int nt = 0; nt < NNT; ++nt) O[mt][nt][r] *= ar;
-        }
-      m_run = mnew;
-    }
-  };
-  auto softmax_pv = [&](int kt, float (&sv)[NSB][16]) {
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sv[sb][r] = fast_exp2(fmaf(sv[sb][r], c, -m_run));
-    const uint16_t* Vb = Vs + (kt & 1) * VBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) pv16_block<NNT>(O, Vb, sb * 32, sv[sb], lane);
-  };
-
-  // prologue: K0, V0 and K1 in LDS; S(0) and its rescale decision
-  load_k(0);
-  load_v(0);
-  write_k(0);
-  write_v(0);
-  if (ntiles > 1) {
-    load_k(1);
-    write_k(1);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();
-  float sA[NSB][16], sB[NSB][16];
-  qk(0, sA);
-  decide(sA);
-  auto iter = [&](int t, float (&cur)[NSB][16], float (&nxt)[NSB][16]) {
-    const bool more = t + 1 < ntiles;
-    if (t + 2 < ntiles) load_k(t + 2);
-    if (more) load_v(t + 1);
-    if (more) qk(t + 1, nxt);      // MFMA ...
-    softmax_pv(t, cur);            // ... beside the exponentials, then P V
-    if (more) decide(nxt);         // row max of t+1 beside P V
-    if (t + 2 < ntiles) write_k(t & 1);
-    if (more) write_v((t + 1) & 1);
-    __syncthreads();
-  };
-  int t = 0;
-  for (; t + 1 < ntiles; t += 2) {
-    iter(t, sA, sB);
-    iter(t + 1, sB, sA);
-  }
-  if (t < ntiles) iter(t, sA, sB);
-
-  IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
-  const int dcol = lane & 15;
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float l = __shfl(O[mt][kLnt][r], (lane & 48) | kLcol);
-      const float inv = 1.f / l;
-      const int q = p0w + 16 * mt + 4 * g16 + r;
-      if (q < a.P) {
-#pragma unroll
-        for (int nt = 0; nt < NNT; ++nt) {
-          const int d = nt * 16 + dcol;
-          if (d < D) {
-            const float v = O[mt][nt][r] * inv;
-            if constexpr (sizeof(IO) == 2) op[(int64_t)q * a.ldo + d] = f2bf(v);
-            else op[(int64_t)q * a.ldo + d] = v;
-          }
-        }
-      }
-    }
 }
 
 // ====================================================================== stored self maps
@@ -1834,69 +1267,35 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
-template <typename IO, typename MQ, int D, int BK, int W>
-static void launch_fused16(const SelfArgs& a, hipStream_t st) {
-  SelfArgs b = a;
-  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
-  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_fused16_kernel<IO, MQ, D, BK, W>), grid, block, 0, st, b);
-}
-
-template <typename IO, typename MQ, int D, int BK, int W, int QB, bool STREAM = false, int SCHED = 0>
+template <typename IO, typename MQ, int D, int BK, int W, int QB>
 static void launch_multi(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, STREAM, SCHED>), grid, block, 0, st, b);
-}
-
-template <typename IO, typename MQ, int D, int BK, int W>
-static void launch_pipe(const SelfArgs& a, hipStream_t st) {
-  SelfArgs b = a;
-  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
-  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_pipe_kernel<IO, MQ, D, BK, W>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
   if constexpr (MP::kElemBytes == 2 && D == 40) {
-    // d = 40 on the bf16 pipe, nothing but O wanted: the 16x16-PV kernels (experiments build,
-    // P2P_SELF_VARIANT 10 / 11: fused16 8 / 4 waves; 12 / 13 / 14: pipelined BK 32 x 8 waves,
-    // 64 x 4, 64 x 8)
+    // d = 40 on the bf16 pipe, nothing but O wanted (G1/G7 without kept maps or autograd):
+    // two 32-row query blocks per wave, 128-key tiles, 8-wave workgroups -- 512 queries per
+    // workgroup, so only where that still fills the grid (P >= 2048).  Experiments build
+    // (P2P_SELF_VARIANT): 16 = the 64-key kernel with the per-tile max, 29 = the same without
+    // (NOMAX), 27 = 256-key tiles, 28 = 4-wave workgroups, 17 = 64-key tiles x 4 waves.
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
-      // production: two 32-row query blocks per wave, 128-key tiles, 8-wave workgroups (512
-      // queries each: only where that still gives >= 4 workgroups per CU row of the grid)
       if (a.variant == 0 && a.P >= 2048) {
-        launch_multi<IO, MQ, D, 128, 8, 2, true>(a, st);
+        launch_multi<IO, MQ, D, 128, 8, 2>(a, st);
         return hipGetLastError();
       }
       switch (a.variant) {
-        case 27:
-          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, true>(a, st); return hipGetLastError(); }
-          break;
-        case 28: launch_multi<IO, MQ, D, 128, 4, 2, true>(a, st); return hipGetLastError();
-        case 10: launch_fused16<IO, MQ, D, 64, 8>(a, st); return hipGetLastError();
-        case 11: launch_fused16<IO, MQ, D, 64, 4>(a, st); return hipGetLastError();
         case 17: launch_multi<IO, MQ, D, 64, 4, 2>(a, st); return hipGetLastError();
-        case 18: launch_multi<IO, MQ, D, 64, 8, 2>(a, st); return hipGetLastError();
-        case 19: launch_multi<IO, MQ, D, 32, 4, 2>(a, st); return hipGetLastError();
-        case 20: launch_multi<IO, MQ, D, 64, 4, 1>(a, st); return hipGetLastError();
-        case 21: launch_multi<IO, MQ, D, 64, 8, 2, true>(a, st); return hipGetLastError();
-        case 22: launch_multi<IO, MQ, D, 64, 4, 2, true>(a, st); return hipGetLastError();
-        case 23: launch_multi<IO, MQ, D, 128, 8, 2, true>(a, st); return hipGetLastError();
-        case 24: launch_multi<IO, MQ, D, 64, 8, 2, false, 1>(a, st); return hipGetLastError();
-        case 25: launch_multi<IO, MQ, D, 64, 8, 2, false, 2>(a, st); return hipGetLastError();
-        case 26: launch_multi<IO, MQ, D, 64, 4, 2, false, 1>(a, st); return hipGetLastError();
+        case 27:
+          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2>(a, st); return hipGetLastError(); }
+          break;
+        case 28: launch_multi<IO, MQ, D, 128, 4, 2>(a, st); return hipGetLastError();
         default: break;
-      }
-      if (a.variant >= 12 && a.variant <= 15 && a.K % 64 == 0) {
-        if (a.variant == 12) launch_pipe<IO, MQ, D, 32, 8>(a, st);
-        else if (a.variant == 13) launch_pipe<IO, MQ, D, 64, 4>(a, st);
-        else if (a.variant == 14) launch_pipe<IO, MQ, D, 64, 8>(a, st);
-        else launch_pipe<IO, MQ, D, 32, 4>(a, st);
-        return hipGetLastError();
       }
     }
   }
