@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 10
+#define P2P_ABI_VERSION 11
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -106,6 +106,20 @@ typedef struct {
   int32_t flags;   /* P2P_PROGRAM_F_* of program (host-known: sizes the launch's LDS) */
   int32_t n_edits; /* edit records the program holds (its header[0]); a group with
                       count - 1 > n_edits is rejected (P2P_E_BATCH) before any launch */
+  /* LocalBlend's word reduction folded into the store epilogue (null_text.py:41-46,
+   * main.py:37-44: (maps * alpha).sum(-1) of the five 16x16 cross layers), nullable: for entry
+   * b of the group, head h and query row p
+   *   blend_sums[((b * 2 + s) * blend_lh + blend_col + h) * n_query + p]  = / +=
+   *       sum_w P'[p][w] * alpha_s[b][w],   alpha_0 = blend_alpha, alpha_1 = blend_sub (or 0)
+   * with P' the post-edit probabilities the store receives, written when store_accumulate = 0
+   * and added otherwise -- the running sum of the word sums, which is what p2p_localblend
+   * (word_sums_ready) reads instead of re-reading the maps.  Needs every entry of the group to
+   * store (store_slot >= 0). */
+  float* blend_sums;
+  const float* blend_alpha; /* [count][n_key] f32                                          */
+  const float* blend_sub;   /* [count][n_key] f32 or NULL                                  */
+  int32_t blend_col;        /* this layer's first column (layer index * n_heads)            */
+  int32_t blend_lh;         /* columns of the sums: blended layers * n_heads                */
 } p2p_group;
 
 /* Cross-attention (ptp_utils.py:183-208 with context=...) with the controller's cross edit
@@ -167,6 +181,9 @@ typedef struct {
   int32_t channels, lat_h, lat_w;
   float* word_sums;                /* workspace [n_prompts, 2, n_maps*heads, res*res]  */
   uint8_t* mask_out;               /* optional [n_prompts, lat_h, lat_w] final mask    */
+  int32_t word_sums_ready;         /* 1: word_sums already hold the word reductions (the
+                                      running sums folded by p2p_cross_attn_fwd's
+                                      blend_sums); maps are then not read (may be NULL)   */
 } p2p_blend_args;
 
 /* x_t may be NULL when mask_out is given: the mask is computed and nothing is blended (the

@@ -1201,6 +1201,19 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       }
     __syncthreads();
     const int rows = min(32, a.P - p0w);
+    // LocalBlend's word sums of these rows (lanes 0-31: alpha, 32-63: substruct), folded here so
+    // the blend never re-reads the maps; words summed in index order as blend_wordsum_kernel does
+    if (a.grp_bsum[gi] != nullptr && qi < rows) {
+      const float* tab = hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi];
+      float acc = 0.f;
+      if (tab != nullptr) {
+        tab += (int64_t)b * K;
+        const float* row = slab + qi * K;
+        for (int w = 0; w < K; ++w) acc += row[w] * tab[w];
+      }
+      float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w + qi;
+      *dst = a.store_accumulate ? *dst + acc : acc;
+    }
     if (rows > 0) {
       float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int count = rows * K;

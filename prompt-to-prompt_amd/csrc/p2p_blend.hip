@@ -279,9 +279,9 @@ int run_localblend(const p2p_blend_args& a, hipStream_t st) {
       a.lat_h < 1 || a.lat_w < 1)
     return P2P_E_ARG;
   for (int l = 0; l < a.n_maps; ++l)
-    if (!a.maps[l]) return P2P_E_ARG;
+    if (!a.maps[l] && !a.word_sums_ready) return P2P_E_ARG;
   dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map, (a.map_res * a.map_res + kWsPix - 1) / kWsPix);
-  hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
+  if (!a.word_sums_ready) hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
   hipLaunchKernelGGL(blend_finalize_kernel, dim3(a.n_prompts), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -136,6 +136,14 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     a.grp_prog[g] = G.program;
     a.grp_alpha[g] = G.alpha;
     a.grp_flags[g] = G.program ? G.flags : 0;
+    a.grp_bsum[g] = G.blend_sums;
+    a.grp_balpha[g] = G.blend_alpha;
+    a.grp_bsub[g] = G.blend_sub;
+    a.grp_bcol[g] = G.blend_col;
+    a.grp_blh[g] = G.blend_lh;
+    if (G.blend_sums && (!G.blend_alpha || G.blend_lh < 1 || G.blend_col < 0 ||
+                         G.blend_col + t->n_heads > G.blend_lh))
+      return P2P_E_ARG;
     for (int e = G.first; e < G.first + G.count; ++e) {
       if (a.ent_group[e] >= 0) return P2P_E_BATCH;  // groups overlap
       a.ent_group[e] = g;
@@ -148,6 +156,11 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     a.store_slot[n] = (store && store_slot) ? store_slot[n] : -1;
     any_store |= a.store_slot[n] >= 0;
   }
+  // folded LocalBlend sums ride on the store epilogue: every entry of such a group must store
+  for (int g = 0; g < n_groups; ++g)
+    if (groups[g].blend_sums)
+      for (int e = groups[g].first; e < groups[g].first + groups[g].count; ++e)
+        if (a.store_slot[e] < 0) return P2P_E_ARG;
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;
   a.any_store = any_store ? 1 : 0;

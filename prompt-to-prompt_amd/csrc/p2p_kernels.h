@@ -54,6 +54,11 @@ struct CrossArgs {
   const void* grp_prog[P2P_MAX_GROUPS];
   const float* grp_alpha[P2P_MAX_GROUPS];
   int grp_flags[P2P_MAX_GROUPS];
+  float* grp_bsum[P2P_MAX_GROUPS];         // LocalBlend word sums (p2p_group.blend_*)
+  const float* grp_balpha[P2P_MAX_GROUPS];
+  const float* grp_bsub[P2P_MAX_GROUPS];
+  int grp_bcol[P2P_MAX_GROUPS];
+  int grp_blh[P2P_MAX_GROUPS];
 };
 
 enum { MODE_FUSED_ = 0, MODE_PV_ = 3 };

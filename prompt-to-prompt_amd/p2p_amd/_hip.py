@@ -31,7 +31,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class HipError(RuntimeError):
@@ -55,7 +55,8 @@ class AttnTensors(ctypes.Structure):
 class Group(ctypes.Structure):
     _fields_ = [("first", ctypes.c_int32), ("count", ctypes.c_int32),
                 ("program", ctypes.c_void_p), ("alpha", ctypes.c_void_p), ("flags", ctypes.c_int32),
-                ("n_edits", ctypes.c_int32)]
+                ("n_edits", ctypes.c_int32), ("blend_sums", ctypes.c_void_p), ("blend_alpha", ctypes.c_void_p),
+                ("blend_sub", ctypes.c_void_p), ("blend_col", ctypes.c_int32), ("blend_lh", ctypes.c_int32)]
 
 
 class BlendArgs(ctypes.Structure):
@@ -66,6 +67,7 @@ class BlendArgs(ctypes.Structure):
         ("th_pool", ctypes.c_float), ("th_sub", ctypes.c_float),
         ("x_t", ctypes.c_void_p), ("channels", ctypes.c_int32), ("lat_h", ctypes.c_int32),
         ("lat_w", ctypes.c_int32), ("word_sums", ctypes.c_void_p), ("mask_out", ctypes.c_void_p),
+        ("word_sums_ready", ctypes.c_int32),
     ]
 
 
@@ -227,15 +229,28 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
 
 def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, store_slot=None,
                accumulate=False):
-    """groups: list of (first, count, program_tensor|None, alpha_tensor|None)."""
+    """groups: list of (first, count, program_tensor|None, alpha_tensor|None[, blend]) with blend =
+    None or (sums [count, 2, lh, n_query] f32, alpha [count, n_key] f32, sub [count, n_key] | None,
+    col, lh): LocalBlend's word sums folded into the store epilogue (p2p_group.blend_*)."""
     t = make_tensors(q, k, v, o, heads, scale, compute)
     G = (Group * len(groups))()
-    for i, (first, count, prog, alpha) in enumerate(groups):
+    for i, grp in enumerate(groups):
+        first, count, prog, alpha = grp[:4]
+        blend = grp[4] if len(grp) > 4 else None
         G[i].first, G[i].count = int(first), int(count)
         G[i].program = prog.data_ptr() if prog is not None else None
         G[i].alpha = alpha.data_ptr() if alpha is not None else None
         G[i].flags = int(getattr(prog, "p2p_flags", 0)) if prog is not None else 0
         G[i].n_edits = int(getattr(prog, "p2p_n_edits", 0)) if prog is not None else 0
+        if blend is not None:
+            sums, balpha, bsub, col, lh = blend
+            _require_cuda(sums, balpha, bsub)
+            assert sums.dtype == torch.float32 and sums.is_contiguous() and sums.numel() == count * 2 * lh * t.n_query
+            assert balpha.dtype == torch.float32 and balpha.is_contiguous() and balpha.shape == (count, t.n_key)
+            assert bsub is None or (bsub.dtype == torch.float32 and bsub.is_contiguous() and bsub.shape == balpha.shape)
+            G[i].blend_sums, G[i].blend_alpha = sums.data_ptr(), balpha.data_ptr()
+            G[i].blend_sub = bsub.data_ptr() if bsub is not None else None
+            G[i].blend_col, G[i].blend_lh = int(col), int(lh)
     slots = _i32_array(store_slot) if store_slot is not None else None
     if store is not None:
         _require_cuda(store)
@@ -270,8 +285,9 @@ def attn_pv(probs, v, o, heads, compute="bf16"):
 
 
 def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_sub, x_t, word_sums,
-               mask_out=None):
-    """LocalBlend on device; x_t None with mask_out given = mask only (no blend)."""
+               mask_out=None, word_sums_ready=False):
+    """LocalBlend on device; x_t None with mask_out given = mask only (no blend).  word_sums_ready:
+    word_sums already holds the folded word reductions (cross_attn blend); the maps are not read."""
     _require_cuda(x_t, alpha_layers, word_sums, substruct_layers, mask_out, *maps)
     a = BlendArgs()
     for i, m in enumerate(maps):
@@ -296,6 +312,7 @@ def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_
         a.channels, a.lat_h, a.lat_w = 0, mask_out.shape[-2], mask_out.shape[-1]
     a.word_sums = word_sums.data_ptr()
     a.mask_out = mask_out.data_ptr() if mask_out is not None else None
+    a.word_sums_ready = int(bool(word_sums_ready))
     rc = lib().p2p_localblend(ctypes.byref(a), _stream((x_t if x_t is not None else mask_out).device))
     _check(rc, "p2p_localblend")
 

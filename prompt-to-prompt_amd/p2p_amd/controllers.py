@@ -80,17 +80,23 @@ def fused_local_blend(x_t, attention_store, alpha_flat, sub_flat, th_pool, th_su
     return out.to(x_t.dtype)
 
 
-def fused_blend_mask(attention_store, alpha_flat, sub_flat, th_pool, th_sub, size):
+def fused_blend_mask(attention_store, alpha_flat, sub_flat, th_pool, th_sub, size, folded=None):
     """LocalBlend's final mask [B, H, W] (uint8) only; the latent blend itself then runs inside
-    p2p_latent_step together with the CFG combine and the DDIM step."""
+    p2p_latent_step together with the CFG combine and the DDIM step.  ``folded``: the running word
+    sums [B, 2, 5 * heads, 256] that the cross-attention store epilogue accumulated
+    (AttentionControlEdit._blend_fold) -- then the 12.6 MB of maps are not re-read."""
     maps = list(attention_store["down_cross"][2:4]) + list(attention_store["up_cross"][:3])
     B = alpha_flat.shape[0]
     if len(maps) != 5:
         raise ValueError(f"LocalBlend needs 2 down and 3 up 16x16 cross maps, store has {len(maps)}")
     heads = maps[0].shape[0] // B
-    maps = [m if (m.dtype == torch.float32 and m.is_contiguous()) else m.float().contiguous() for m in maps]
     dev = maps[0].device
     mask = torch.empty(B, *size, dtype=torch.uint8, device=dev)
+    if folded is not None:
+        _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, None, folded, mask_out=mask,
+                        word_sums_ready=True)
+        return mask
+    maps = [m if (m.dtype == torch.float32 and m.is_contiguous()) else m.float().contiguous() for m in maps]
     ws = torch.empty(B * 2 * len(maps) * heads * maps[0].shape[1], dtype=torch.float32, device=dev)
     _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, None, ws, mask_out=mask)
     return mask
@@ -121,11 +127,16 @@ class LocalBlend:
             raise ValueError("main-form LocalBlend broadcasts only for 2 prompts (see null_text.LocalBlend)")
         return fused_local_blend(x_t, attention_store, self._alpha_flat, None, self.threshold, self.threshold)
 
-    def step_mask(self, attention_store, size):
+    def step_mask(self, attention_store, size, folded=None):
         """The blend mask __call__ would apply this step (fused latent-step protocol)."""
         if self.alpha_layers.shape[0] != 2:
             raise ValueError("main-form LocalBlend broadcasts only for 2 prompts (see null_text.LocalBlend)")
-        return fused_blend_mask(attention_store, self._alpha_flat, None, self.threshold, self.threshold, size)
+        return fused_blend_mask(attention_store, self._alpha_flat, None, self.threshold, self.threshold, size,
+                                folded)
+
+    def _fold_tables(self):
+        """(alpha [B, W], substruct [B, W] or None) the store epilogue folds the word sums with."""
+        return self._alpha_flat, None
 
     def __init__(self, prompts: List[str], words, threshold=.3, tokenizer=None, device=None):
         tokenizer = tokenizer or get_tokenizer()
@@ -307,6 +318,7 @@ class AttentionStore(AttentionControl):
         key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
         idx = self._fused_calls[key]
         self._fused_calls[key] = idx + 1
+        self._last_store_key = (key, idx)
         if len(self.attention_store) == 0:
             t = torch.empty(n_cond * heads, P, K, dtype=torch.float32, device=device)
             self.step_store[key].append(t)
@@ -354,7 +366,47 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
             return None
         if not (_owned(lb, "__call__") and hasattr(lb, "step_mask")):
             raise NotFusable
-        return lambda size: lb.step_mask(self.attention_store, size)
+        return lambda size: lb.step_mask(self.attention_store, size,
+                                         folded=self._blend_sums if self._blend_valid else None)
+
+    # LocalBlend's word reduction folded into the cross-attention store epilogue: the five 16x16
+    # cross layers it reads (main.py:37-38, down_cross[2:4] + up_cross[:3]) get their running word
+    # sums accumulated by the kernel that writes their maps, so the blend reads ~0.3 MB instead
+    # of the 12.6 MB of maps every step.  Valid only while EVERY step folded all five layers.
+    BLEND_SLOTS = {("down_cross", 2): 0, ("down_cross", 3): 1, ("up_cross", 0): 2, ("up_cross", 1): 3,
+                   ("up_cross", 2): 4}
+
+    def _blend_fold(self, key_idx, P, K, heads, device):
+        """The p2p_group.blend_* tuple for this stored cross layer, or None."""
+        lb = self.local_blend
+        slot = self.BLEND_SLOTS.get(key_idx)
+        if slot is None or lb is None or P != 256 or not (_owned(lb, "__call__") and hasattr(lb, "_fold_tables")):
+            return None
+        alpha, sub = lb._fold_tables()
+        if alpha.shape != (self.batch_size, K) or alpha.device != device:
+            return None
+        lh = len(self.BLEND_SLOTS) * heads
+        if len(self.attention_store) == 0 and slot == 0:
+            self._blend_sums = torch.empty(self.batch_size, 2, lh, P, dtype=torch.float32, device=device)
+            self._blend_valid = False
+            self._blend_step = set()
+        if self._blend_sums is None or self._blend_sums.shape != (self.batch_size, 2, lh, P):
+            return None
+        self._blend_step.add(slot)
+        return self._blend_sums, alpha, sub, slot * heads, lh
+
+    def between_steps(self):
+        # a step in which some blend layer did not fold (materialised protocol, a new run) ends
+        # the folded sums' validity until the next reset
+        first = len(self.attention_store) == 0
+        complete = self._blend_sums is not None and len(self._blend_step) == len(self.BLEND_SLOTS)
+        self._blend_valid = complete and (first or self._blend_valid)
+        self._blend_step = set()
+        super().between_steps()
+
+    def reset(self):
+        super().reset()
+        self._blend_sums, self._blend_valid, self._blend_step = None, False, set()
 
     def fused_step_mask(self):
         try:
@@ -406,6 +458,7 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         self.num_self_replace = int(num_steps * self_replace_steps[0]), int(num_steps * self_replace_steps[1])
         self.local_blend = local_blend
         self._program_cache = {}
+        self._blend_sums, self._blend_valid, self._blend_step = None, False, set()
 
     # ------------------------------------------------------------------ fused edits
     def _edit_program(self) -> programs.EditProgram:
@@ -435,7 +488,8 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         slots = self._slots(N, n0, heads, store)
         out = torch.empty_like(q)
         if is_cross:
-            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous())]
+            blend = self._blend_fold(self._last_store_key, P, K, heads, q.device) if store is not None else None
+            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous(), blend)]
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
                             store_slot=slots, accumulate=acc)
         else:
@@ -635,7 +689,7 @@ class GroupBatch(AttentionControl):
         GB = G * B
         if N != 2 * GB:
             raise ValueError(f"GroupBatch of {G} x {B} prompts got a U-Net batch of {N}")
-        store, acc, slots = None, False, None
+        store, acc, slots, store_key = None, False, None, None
         store_self = self._storing and all(m.store_self_maps for m in self.members)
         if self._storing and not is_cross and any(m.store_self_maps for m in self.members) and not store_self:
             raise ValueError("GroupBatch members disagree on store_self_maps")
@@ -643,6 +697,7 @@ class GroupBatch(AttentionControl):
             key = f"{place_in_unet}_{'cross' if is_cross else 'self'}"
             idx = self._calls[key]
             self._calls[key] = idx + 1
+            store_key = (key, idx)
             if len(self.members[0].attention_store) == 0:
                 store = torch.empty(GB * heads, P, K, dtype=torch.float32, device=q.device)
                 for g, m in enumerate(self.members):
@@ -660,7 +715,8 @@ class GroupBatch(AttentionControl):
                     alpha = m.cross_replace_alpha[m.cur_step]
                     if alpha.shape[-1] != K or alpha.device != q.device:
                         raise ValueError("edit tables do not match this attention call")
-                    groups.append((first, B, m._device_program(q.device), alpha.contiguous()))
+                    blend = m._blend_fold(store_key, P, K, heads, q.device) if store is not None else None
+                    groups.append((first, B, m._device_program(q.device), alpha.contiguous(), blend))
                 else:
                     groups.append((first, B, None, None))
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,

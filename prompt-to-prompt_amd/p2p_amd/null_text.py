@@ -51,15 +51,21 @@ class LocalBlend:
             x_t = _c.fused_local_blend(x_t, attention_store, self._alpha_flat, sub, self.th[0], self.th[1])
         return x_t
 
-    def step_mask(self, attention_store, size):
+    def step_mask(self, attention_store, size, folded=None):
         """What __call__ does to its counter, returning the mask it would blend with (or None
-        before start_blend) -- the fused latent-step protocol."""
+        before start_blend) -- the fused latent-step protocol.  ``folded``: the running word sums
+        the cross-attention store epilogue accumulated (AttentionControlEdit._blend_fold)."""
         self.counter += 1
         if self.counter > self.start_blend:
             self._size = tuple(size)
             sub = self._sub_flat if self.substruct_layers is not None else None
-            return _c.fused_blend_mask(attention_store, self._alpha_flat, sub, self.th[0], self.th[1], size)
+            return _c.fused_blend_mask(attention_store, self._alpha_flat, sub, self.th[0], self.th[1], size,
+                                       folded)
         return None
+
+    def _fold_tables(self):
+        """(alpha [B, W], substruct [B, W] or None) the store epilogue folds the word sums with."""
+        return self._alpha_flat, (self._sub_flat if self.substruct_layers is not None else None)
 
     def __init__(self, prompts: List[str], words, substruct_words=None, start_blend=0.2, th=(.3, .3),
                  tokenizer=None, device=None):

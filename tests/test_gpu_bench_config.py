@@ -25,8 +25,8 @@ def _record_masks(lb, sink):
     """Wrap the product LocalBlend's per-step mask (fused latent-step protocol) to keep a copy."""
     orig = lb.step_mask
 
-    def step_mask(store, size):
-        m = orig(store, size)
+    def step_mask(store, size, folded=None):
+        m = orig(store, size, folded=folded)
         sink.append(None if m is None else m.clone())
         return m
 
