@@ -54,15 +54,17 @@ def time_fn(fn, iters=50, warm=3):
 
 def main():
     var = int(os.environ.get("P2P_SELF_VARIANT", "0"))
+    P0, d0 = (int(x) for x in os.environ.get("G1AB_SHAPE", "4096,40").split(","))
     errs = {
-        "g1": check(8, 4096, 4096, 40),
-        "peaky16": check(2, 4096, 4096, 40, qscale=16.0),
-        "remap": check(8, 1024, 1024, 40, qk_src=[0, 1, 2, 3, 4, 4, 4, 4]),
-        "ragged": check(2, 1000, 777, 40),
-        "f32in": check(2, 2048, 2048, 40, dtype=torch.float32),
+        "g1": check(8, P0, P0, d0),
+        "peaky16": check(2, P0, P0, d0, qscale=16.0),
+        "remap": check(8, 1024, 1024, d0, qk_src=[0, 1, 2, 3, 4, 4, 4, 4]),
+        "ragged": check(2, 1000, 777, d0),
+        "f32in": check(2, 2048, 2048, d0, dtype=torch.float32),
     }
     ok = all(e < 2.0 ** -7 * 2 for e in errs.values())
-    N, H, P, d = 8, 8, 4096, 40
+    P, d = (int(x) for x in os.environ.get("G1AB_SHAPE", "4096,40").split(","))
+    N, H = 8, 8
     C = H * d
     q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
     k = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the dominant kernel (tools/g1_only.py), one rocprofv3 run per counter group
 # (gfx950 slot limits: 8 SQ, 4 TCC -- FETCH_SIZE alone uses 3).  Output: gpurun_out/pmc/<tag>_<pass>/
-# Usage: tools/gpu_pmc.sh <tag> [extra args for g1_only.py]
+# Usage: [PMC_SCRIPT=tools/x.py] tools/gpu_pmc.sh <tag> [extra args for the script (default tools/g1_only.py)]
 set -u
 tag=${1:-cur}; shift || true
 export TMPDIR=/tmp
@@ -17,7 +17,7 @@ i=0
 for p in "${passes[@]}"; do
   i=$((i+1))
   d=$out/${tag}_p$i
-  timeout -s KILL 90 rocprofv3 --pmc $p --output-format csv -d $d -o run -- python3 tools/g1_only.py "$@" > $d.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $p --output-format csv -d $d -o run -- python3 ${PMC_SCRIPT:-tools/g1_only.py} "$@" > $d.log 2>&1
   rc=$?
   echo "pass $i ($p) rc=$rc"
   if [ $rc -ge 124 ]; then tail -5 $d.log; exit $rc; fi
