@@ -435,12 +435,24 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 // defer-max rule -- the sub-block's P V follows at once, so no P is pending at a rescale.
 // Measured at G1 (N = 8, H = 8, bf16; tools/g1_ab.py, profiles/r02): 0.239 ms (64-key tiles with
 // the per-tile max, one block per wave) -> 0.233 (NOMAX) -> 0.217 (this, QB = 2, BK = 128).
-template <typename IO, typename MQ, int D, int BK, int WAVES, int QB>
+//
+// F16 (bf16 inputs, d = 40): the MFMA itself emits the exponent c*s - m, so a score costs one
+// v_exp and half a v_cvt_pk on the VALU instead of v_fma + v_exp + half a cvt:
+//   * Q is prescaled by c = scale*log2(e) once, at load, and rounded to f16 (2^-12 relative,
+//     8x finer than bf16); K is staged as f16 -- exact, a bf16 value has 8 significant bits --
+//     so the QK^T products stay exact in the f32 accumulator;
+//   * d = 40 pads to 48 for the MFMA: K column 40 is 1 and Q column 40 holds -m (the row's
+//     reference point, an f16 value), so S^T = c s - m comes out of the MFMA;
+//   * values outside the f16 range (|k| >= 65520, |c q| >= 65520, |m| >= 65504) set a flag and
+//     the workgroup recomputes on the exact bf16 path (K restaged as bf16, fma with c), like the
+//     NOMAX overflow recompute.
+template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool F16 = false>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   static_assert(DV > D, "needs the ones column");
+  static_assert(!F16 || (DK > D && MQ::planes == 1 && sizeof(IO) == 2), "F16: bf16 inputs, a padding column");
   constexpr int NKT = DK / 16;
   constexpr int NDT = DV / 32;
   constexpr int NSB = BK / 32;
@@ -458,6 +470,10 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   constexpr int kLrr = D % 32;
   constexpr int kLh = (kLrr >> 2) & 1;
   constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+  // F16: Q column D (the -m slot) = element (D % 16) % 8 of k-step D / 16, lane half (D % 16) / 8
+  constexpr int kMt = D / 16;
+  constexpr int kMh = (D % 16) / 8;
+  constexpr int kMj = D % 8;
   constexpr float kRescaleThr = 8.0f;
   __shared__ __attribute__((aligned(16))) char smem[KBYTES + VBYTES + 16];
   __shared__ int wg_bad;
@@ -487,17 +503,35 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   for (int i = tid; i < (KBYTES + VBYTES) / 4; i += NT) reinterpret_cast<float*>(smem)[i] = 0.f;
   if (tid == 0) wg_bad = 0;
   __syncthreads();
-  for (int r = tid; r < 2 * BK; r += NT) Vs[r * VS + D] = 0x3F80;
+  for (int r = tid; r < 2 * BK; r += NT) {
+    Vs[r * VS + D] = 0x3F80;
+    if constexpr (F16) Ks[r * KS + D] = 0x3C00;   // f16 1.0: the -m column of Q K^T
+  }
 
+  // F16 state: the exact bf16 path is taken by the recompute only (ex), after an f16 range miss
+  bool ovf = false;
   typename MQ::frag qf[QB][NKT];
+  auto load_qf = [&](auto ex) __attribute__((always_inline)) {
 #pragma unroll
-  for (int b = 0; b < QB; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      const int col = 16 * t + 8 * hh;
-      const int p = pw + 32 * b + qi;
-      qf[b][t] = (p < a.P && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
-    }
+      for (int t = 0; t < NKT; ++t) {
+        const int col = 16 * t + 8 * hh;
+        const int p = pw + 32 * b + qi;
+        qf[b][t] = (p < a.P && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+        if constexpr (F16) if constexpr (!decltype(ex)::value) {
+          float mx = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float x = bf2f((uint16_t)qf[b][t].h[j]) * c;
+            mx = fmaxf(mx, fabsf(x));
+            qf[b][t].h[j] = (short)__builtin_bit_cast(uint16_t, (_Float16)x);
+          }
+          ovf |= !(mx < 65520.f);
+        }
+      }
+  };
+  load_qf(std::false_type{});
 
   Chunk8<IO> kreg[NCH], vreg[NCH];
   uint32_t koff[NCH], voff[NCH];
@@ -513,7 +547,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + D) * (int64_t)sizeof(IO);
   const int64_t kstep = (int64_t)BK * a.ldk * (int64_t)sizeof(IO);
   const int64_t vstep = (int64_t)BK * a.ldv * (int64_t)sizeof(IO);
-  auto stage_load = [&](int kt) {
+  auto stage_load = [&](int kt) __attribute__((always_inline)) {
     const __amdgpu_buffer_rsrc_t rk =
         make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
     const __amdgpu_buffer_rsrc_t rv =
@@ -526,14 +560,33 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
       }
     }
   };
-  auto stage_write = [&](int buf) {
+  auto stage_write = [&](int buf, auto ex) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       if ((BK * CPR) % NT == 0 || cidx < BK * CPR) {
         const int row = cidx / CPR;
         const int ch = cidx - row * CPR;
-        MQ::stage(kreg[i], Ks + buf * KBUF + row * KS + ch * 8, KPLANE);
+        EK* const kd = Ks + buf * KBUF + row * KS + ch * 8;
+        bool staged = false;
+        if constexpr (F16) if constexpr (!decltype(ex)::value) {
+          staged = true;
+          // bf16 -> f16 is exact inside the f16 range (8 significant bits); RTZ packing, so a
+          // value past 65504 would clamp silently: range-checked instead
+          short8_t hv;
+          float mx = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const float x0 = bf2f((uint16_t)kreg[i].v[j]), x1 = bf2f((uint16_t)kreg[i].v[j + 1]);
+            mx = fmaxf(mx, fmaxf(fabsf(x0), fabsf(x1)));
+            const auto pk = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x0, x1));
+            hv[j] = (short)(pk & 0xffff);
+            hv[j + 1] = (short)(pk >> 16);
+          }
+          ovf |= !(mx < 65504.f);
+          *reinterpret_cast<short8_t*>(kd) = hv;
+        }
+        if (!staged) MQ::stage(kreg[i], kd, KPLANE);
         vreg[i].store(Vs + buf * VBUF + row * VS + ch * 8);
       }
     }
@@ -542,22 +595,42 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   const int ntiles = (K + BK - 1) / BK;
   f32x16_t O[QB][NDT];
   float m_run[QB];
+  float m_q[QB];   // F16: the reference point currently held in Q column D (as -m)
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     m_run[b] = -INFINITY;
+    m_q[b] = 0.f;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) O[b][dt] = f32x16_t{};
   }
+  auto set_mcol = [&](int b, float m) __attribute__((always_inline)) {   // F16: Q column D := -m (lanes of half kMh)
+    m_q[b] = m;
+    if constexpr (F16)
+      if (hh == kMh) qf[b][kMt].h[kMj] = (short)__builtin_bit_cast(uint16_t, (_Float16)(-m));
+  };
+  auto mma_qk = [&](f32x16_t& acc, const typename MQ::frag& k, const typename MQ::frag& q, auto ex)
+      __attribute__((always_inline)) {
+    bool done = false;
+    if constexpr (F16) if constexpr (!decltype(ex)::value) {
+      done = true;
+      typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, k.h),
+                                                   __builtin_bit_cast(f16x8_t, q.h), acc, 0, 0, 0);
+    }
+    if (!done) MQ::mma(acc, k, q);
+  };
 
   stage_load(0);
-  stage_write(0);
+  stage_write(0, std::false_type{});
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   bool bad = false;
   // One tile, sub-block by sub-block (Q K^T, [max decision], exp, P V): only one sub-block's scores
   // per query block are live.  Slow tiles (the first one, and the overflow recompute) move the
   // reference point per 32-key sub-block with the defer-max rule; fast tiles (NOMAX) do not.
-  auto tile = [&](int kt, auto masked, auto fast) {
+  // ex: the exact bf16 path (F16 recompute after a range miss; the only path without F16).
+  auto tile = [&](int kt, auto masked, auto fast, auto ex) __attribute__((always_inline)) {
+    constexpr bool kF16 = F16 && !decltype(ex)::value;
     const int buf = kt & 1;
     if (kt + 1 < ntiles) stage_load(kt + 1);
     const EK* Kb = Ks + buf * KBUF;
@@ -571,7 +644,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
       for (int t = 0; t < NKT; ++t) {
         const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
 #pragma unroll
-        for (int b = 0; b < QB; ++b) MQ::mma(acc[b], fa, qf[b][t]);
+        for (int b = 0; b < QB; ++b) mma_qk(acc[b], fa, qf[b][t], ex);
       }
       float sv[QB][16];
 #pragma unroll
@@ -588,9 +661,14 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
           float mx = -INFINITY;
 #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[b][r]);
-          mx = fmaxf(mx, other_half(mx)) * c;
+          mx = fmaxf(mx, other_half(mx));
+          mx = kF16 ? mx + m_q[b] : mx * c;   // the sub-block's max, log2 units
           if (__builtin_expect(!__all(mx <= m_run[b] + kRescaleThr), 0)) {
-            const float mnew = fmaxf(m_run[b], mx);
+            float mnew = fmaxf(m_run[b], mx);
+            if constexpr (kF16) {
+              mnew = (float)(_Float16)mnew;   // representable in Q's f16 column
+              ovf |= !(fabsf(mnew) < 65504.f);
+            }
             const float alpha = fast_exp2(m_run[b] - mnew);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt)
@@ -601,9 +679,22 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
         }
       }
 #pragma unroll
-      for (int b = 0; b < QB; ++b)
+      for (int b = 0; b < QB; ++b) {
+        if constexpr (kF16) {
+          if constexpr (decltype(fast)::value) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sv[b][r] = fast_exp2(fmaf(sv[b][r], c, -m_run[b]));
+            for (int r = 0; r < 16; ++r) sv[b][r] = fast_exp2(sv[b][r]);
+          } else {
+            const float dm = m_run[b] - m_q[b];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sv[b][r] = fast_exp2(sv[b][r] - dm);
+            set_mcol(b, m_run[b]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sv[b][r] = fast_exp2(fmaf(sv[b][r], c, -m_run[b]));
+        }
+      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         MmaBf16::frag pb[QB];
@@ -630,19 +721,28 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
 #pragma unroll
               for (int r = 0; r < 16; ++r) O[b][dt][r] *= 0x1p-64f;
             m_run[b] += 64.f;
+            if constexpr (kF16) {
+              ovf |= !(fabsf(m_run[b]) < 65504.f);
+              set_mcol(b, m_run[b]);
+            }
           }
         }
       }
     }
-    if (kt + 1 < ntiles) stage_write(buf ^ 1);
+    if (kt + 1 < ntiles) stage_write(buf ^ 1, ex);
     __syncthreads();
   };
   const int nfull = K / BK;
-  if (nfull == 0) tile(0, std::true_type{}, std::false_type{});
-  else tile(0, std::false_type{}, std::false_type{});
-  for (int kt = 1; kt < nfull; ++kt) tile(kt, std::false_type{}, std::true_type{});
-  if (nfull < ntiles && nfull > 0) tile(nfull, std::true_type{}, std::true_type{});
-  if (__any(bad) && lane == 0) wg_bad = 1;
+  constexpr std::false_type kNo{};
+  constexpr std::true_type kYes{};
+  if (nfull == 0) tile(0, kYes, kNo, kNo);
+  else tile(0, kNo, kNo, kNo);
+  for (int kt = 1; kt < nfull; ++kt) tile(kt, kNo, kYes, kNo);
+  if (nfull < ntiles && nfull > 0) tile(nfull, kYes, kYes, kNo);
+  {
+    const bool any_bad = __any(bad), any_ovf = __any(ovf);
+    if (lane == 0 && (any_bad || any_ovf)) atomicOr(&wg_bad, any_ovf ? 2 : 1);
+  }
   __syncthreads();
   if (__builtin_expect(wg_bad != 0, 0)) {
 #pragma unroll
@@ -651,12 +751,26 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) O[b][dt] = f32x16_t{};
     }
-    stage_load(0);
-    stage_write(0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-    for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{}, std::false_type{});
-    if (nfull < ntiles) tile(nfull, std::true_type{}, std::false_type{});
+    auto redo = [&](auto ex) __attribute__((always_inline)) {
+      if constexpr (decltype(ex)::value) {
+        load_qf(ex);   // unscaled bf16 Q, column D zero
+      } else if constexpr (F16) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) set_mcol(b, 0.f);
+      }
+      stage_load(0);
+      stage_write(0, ex);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
+      for (int kt = 0; kt < nfull; ++kt) tile(kt, kNo, kNo, ex);
+      if (nfull < ntiles) tile(nfull, kYes, kNo, ex);
+    };
+    if constexpr (F16) {
+      if (wg_bad & 2) redo(kYes);
+      else redo(kNo);
+    } else {
+      redo(kNo);
+    }
   }
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
@@ -1280,12 +1394,12 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
-template <typename IO, typename MQ, int D, int BK, int W, int QB>
+template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false>
 static void launch_multi(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
@@ -1295,19 +1409,24 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     // d = 40 on the bf16 pipe, nothing but O wanted (G1/G7 without kept maps or autograd):
     // two 32-row query blocks per wave, 128-key tiles, 8-wave workgroups -- 512 queries per
     // workgroup, so only where that still fills the grid (P >= 2048).  Experiments build
-    // (P2P_SELF_VARIANT): 16 = the 64-key kernel with the per-tile max, 29 = the same without
-    // (NOMAX), 27 = 256-key tiles, 28 = 4-wave workgroups, 17 = 64-key tiles x 4 waves.
+    // (P2P_SELF_VARIANT): 40 = the bf16 form (v_fma per score), 16 = the 64-key kernel with the
+    // per-tile max, 29 = the same without (NOMAX), 27 = 256-key tiles, 28 = 4-wave workgroups,
+    // 17 = 64-key tiles x 4 waves.
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
+      constexpr bool kF16 = MQ::planes == 1 && sizeof(IO) == 2;
       if (a.variant == 0 && a.P >= 2048) {
-        launch_multi<IO, MQ, D, 128, 8, 2>(a, st);
+        // bf16 inputs: the F16 form (scale and reference point inside the MFMA)
+        launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st);
         return hipGetLastError();
       }
       switch (a.variant) {
-        case 17: launch_multi<IO, MQ, D, 64, 4, 2>(a, st); return hipGetLastError();
+        case 40: launch_multi<IO, MQ, D, 128, 8, 2>(a, st); return hipGetLastError();
+        case 17: launch_multi<IO, MQ, D, 64, 4, 2, kF16>(a, st); return hipGetLastError();
         case 27:
-          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2>(a, st); return hipGetLastError(); }
+          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16>(a, st); return hipGetLastError(); }
           break;
-        case 28: launch_multi<IO, MQ, D, 128, 4, 2>(a, st); return hipGetLastError();
+        case 28: launch_multi<IO, MQ, D, 128, 4, 2, kF16>(a, st); return hipGetLastError();
+        case 41: launch_multi<IO, MQ, D, 64, 8, 2, kF16>(a, st); return hipGetLastError();
         default: break;
       }
     }
