@@ -1079,6 +1079,110 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   const int P0S = a.slab_stride;
   float* const slab = reinterpret_cast<float*>(cross_dyn) + wave * 32 * P0S;
 
+  // ---- plain entries (no edit program, maps not kept): the lean path.  Every global load is
+  // issued first (Q fragments, this thread's K and V chunks) and the padding is written while they
+  // fly; V's column D is 1, so the P V MFMA's row D is the row sum of the bf16 weights it used
+  // (no per-element sum, no normalised P: O is scaled once); only a key block that runs past K
+  // is masked.  (Measured at G1, N = 8, H = 8: tools/cross_bench.py, profiles/r02.)
+  if constexpr (MP::kElemBytes == 2 && DV > D) {
+    if (!edit && !(a.store && a.store_slot[n] >= 0)) {
+      constexpr int kLdt = D / 32;
+      constexpr int kLrr = D % 32;
+      constexpr int kLh = (kLrr >> 2) & 1;
+      constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+      typename MQ::frag qf[NKT];
+      {
+        const IO* qp = static_cast<const IO*>(a.q) + (int64_t)n * a.bsq + h * D + (int64_t)p * a.ldq;
+#pragma unroll
+        for (int t = 0; t < NKT; ++t) {
+          const int col = 16 * t + 8 * hh;
+          qf[t] = (prow && col < D) ? MQ::load_q(qp + col) : MQ::zero();
+        }
+      }
+      const IO* kp = static_cast<const IO*>(a.k) + (int64_t)n * a.bsk + h * D;
+      const IO* vp = static_cast<const IO*>(a.v) + (int64_t)n * a.bsv + h * D;
+      Chunk8<IO> kc[NCH], vc[NCH];
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int cidx = tid + i * NT;
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        if (cidx < K * CPR) {
+          kc[i].load(kp + (int64_t)row * a.ldk + ch * 8);
+          vc[i].load(vp + (int64_t)row * a.ldv + ch * 8);
+        }
+      }
+      if constexpr (DK > D) {   // K columns D..DK of every row: Q's zero columns meet zeros, not stale LDS
+        constexpr int PC = (DK - D) / 8;
+        for (int i = tid; i < KR * PC * MQ::planes; i += NT) {
+          const int pl = i / (KR * PC);
+          const int j = i - pl * KR * PC;
+          *reinterpret_cast<short8_t*>(Ks + pl * KPLANE + (j / PC) * KS + D + 8 * (j % PC)) = short8_t{};
+        }
+      }
+      for (int i = tid; i < (KR - K) * VS / 8; i += NT)   // V rows K..KR (weighted by p = 0)
+        *reinterpret_cast<short8_t*>(Vs + K * VS + 8 * i) = short8_t{};
+      for (int r = tid; r < K; r += NT) Vs[r * VS + D] = 0x3F80;   // bf16 1.0: the row-sum column
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int cidx = tid + i * NT;
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        if (cidx < K * CPR) {
+          MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
+          vc[i].store(Vs + row * VS + ch * 8);
+        }
+      }
+      __syncthreads();
+      float sv[KB][16];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        f32x16_t acc = {};
+#pragma unroll
+        for (int t = 0; t < NKT; ++t) {
+          const typename MQ::frag fa = MQ::load_k(Ks + (kb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
+          MQ::mma(acc, fa, qf[t]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[kb][r] = acc[r];
+        if (kb * 32 + 32 > K) {   // wave-uniform: only the block that runs past K
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb * 32 + acc_row(r, hh) >= K) sv[kb][r] = -INFINITY;
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[kb][r]);
+      mx = fmaxf(mx, other_half(mx)) * c;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[kb][r] = fast_exp2(fmaf(sv[kb][r], c, -mx));
+      f32x16_t O[NDT];
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
+      const float inv = 1.f / __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
+      if (prow) {
+        IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int dd = dt * 32 + 8 * g + 4 * hh;
+            if (dd < D)
+              store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
+                     O[dt][4 * g + 3] * inv);
+          }
+      }
+      return;
+    }
+  }
+
   // padding the MFMAs read but the staging never writes (disjoint from it: no extra barrier):
   // K columns D..DK (multiplied by Q's zero columns) and V rows K..KR (weighted by p = 0)
   if constexpr (DK > D) {
@@ -1100,32 +1204,38 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     }
   };
 
-  auto stage = [&](int e, bool withV) {
+  // K (and V) of entry e: global -> registers (load_kv), registers -> LDS (store_kv)
+  auto load_kv = [&](int e, Chunk8<IO> (&kc)[NCH], Chunk8<IO> (&vc)[NCH], bool withV) {
     const IO* kp = static_cast<const IO*>(a.k) + (int64_t)e * a.bsk + h * D;
     const IO* vp = static_cast<const IO*>(a.v) + (int64_t)e * a.bsv + h * D;
-    Chunk8<IO> kc[NCH], vc[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
-      if (cidx < KR * CPR && row < K) {
+      if (cidx < K * CPR) {
         kc[i].load(kp + (int64_t)row * a.ldk + ch * 8);
         if (withV) vc[i].load(vp + (int64_t)row * a.ldv + ch * 8);
       }
     }
+  };
+  auto store_kv = [&](const Chunk8<IO> (&kc)[NCH], const Chunk8<IO> (&vc)[NCH], bool withV) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
-      if (cidx < KR * CPR && row < K) {
+      if (cidx < K * CPR) {
         MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
         if (withV) vc[i].store(Vs + row * VS + ch * 8);
       }
     }
   };
-
+  auto stage = [&](int e, bool withV) {
+    Chunk8<IO> kc[NCH], vc[NCH];
+    load_kv(e, kc, vc, withV);
+    store_kv(kc, vc, withV);
+  };
   // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row (K rows past
   // K hold stale LDS: their accumulator rows are replaced by -inf, never used)
   auto probs = [&](const typename MQ::frag (&qf)[NKT], float (&sv)[KB][16]) {
