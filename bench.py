@@ -245,7 +245,7 @@ def main():
                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "algorithmic_bytes": 4.0 * 8 * G * 4096 * 320 * 2,
-                    "kernel": f"self_attn_multi_kernel G1/G7 (P=K=4096, d=40, N={8 * G}, H=8; 2 x 32 queries per wave, 128-key tiles)",
+                    "kernel": f"self_attn_multi_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 2 x 32 queries per wave, 128-key tiles)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
         cpu = None

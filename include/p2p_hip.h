@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 11
+#define P2P_ABI_VERSION 12
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -31,8 +31,8 @@ extern "C" {
 /* bytes of one edit's record: c_rep f32[COLS] | post f32[COLS] | {i32 row, f32 val}[TMAX][COLS] */
 #define P2P_PROGRAM_REC_BYTES (2 * 4 * P2P_PROGRAM_COLS + 8 * P2P_PROGRAM_TMAX * P2P_PROGRAM_COLS)
 #define P2P_PROGRAM_HEADER_BYTES 32
-#define P2P_PROGRAM_DENSE 96 /* dense mapper tile: bf16 [DENSE][DENSE] per edit             */
-enum { P2P_PROGRAM_F_DENSE = 1 }; /* p2p_group.flags: the program carries the dense bf16 tile */
+#define P2P_PROGRAM_DENSE 96 /* dense mapper tile: f16 [DENSE][DENSE] per edit              */
+enum { P2P_PROGRAM_F_DENSE = 1 }; /* p2p_group.flags: the program carries the dense f16 tile  */
 
 enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };
 enum { P2P_COMPUTE_BF16 = 0, P2P_COMPUTE_F32 = 1 };
@@ -93,11 +93,11 @@ int p2p_self_attn_fwd(const p2p_attn_tensors* t, const int32_t* qk_src, float* s
  * the number of planes the kernel walks:
  *   R[w] = post[w] * (c_rep[w] * P_e[w] + sum_{t < tmax} val[t][w] * P_0[row[t][w]])
  *   P_e'[w] = alpha[w] * R[w] + (1 - alpha[w]) * P_e[w]
- * When every term value is exact in bf16 the program also holds, at byte dense_offset, the
- * dense mapper of each edit as bf16 [P2P_PROGRAM_DENSE rows (source word)][P2P_PROGRAM_DENSE
+ * When every term value is exact in f16 the program also holds, at byte dense_offset, the
+ * dense mapper of each edit as f16 [P2P_PROGRAM_DENSE rows (source word)][P2P_PROGRAM_DENSE
  * cols (target word)] (zeros elsewhere), and the host sets P2P_PROGRAM_F_DENSE in flags: the
- * bf16 kernels then form sum_t val * P_0[row] as the MFMA product P_0 . M_e (P_0 split into
- * two bf16 parts, ~2^-16 relative) instead of an LDS gather.                                */
+ * bf16 kernels then form sum_t val * P_0[row] as one f16 MFMA product P_0 . M_e (P_0 rounded
+ * to 11 significant bits, <= 2^-12 relative) instead of an LDS gather.  (ABI 12: f16 tile.)  */
 typedef struct {
   int32_t first;
   int32_t count;

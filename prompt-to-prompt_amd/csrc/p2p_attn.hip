@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 //   * values outside the f16 range (|k| >= 65520, |c q| >= 65520, |m| >= 65504) set a flag and
 //     the workgroup recomputes on the exact bf16 path (K restaged as bf16, fma with c), like the
 //     NOMAX overflow recompute.
-template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool F16 = false>
+template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool F16 = false, bool PIPE = false>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   constexpr int DK = (D + 15) / 16 * 16;
@@ -635,9 +635,7 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
     if (kt + 1 < ntiles) stage_load(kt + 1);
     const EK* Kb = Ks + buf * KBUF;
     const uint16_t* Vb = Vs + buf * VBUF;
-#pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      f32x16_t acc[QB];
+    auto qk = [&](int sb, f32x16_t (&acc)[QB]) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < QB; ++b) acc[b] = f32x16_t{};
 #pragma unroll
@@ -645,6 +643,22 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
         const typename MQ::frag fa = MQ::load_k(Kb + (sb * 32 + qi) * KS + 16 * t + 8 * hh, KPLANE);
 #pragma unroll
         for (int b = 0; b < QB; ++b) mma_qk(acc[b], fa, qf[b][t], ex);
+      }
+    };
+    // PIPE (fast F16 tiles, where the reference point is fixed for the whole tile): sub-block
+    // sb+1's Q K^T is issued before sub-block sb's exponentials, so they can overlap it
+    constexpr bool kPipe = PIPE && kF16 && decltype(fast)::value;
+    f32x16_t accs[2][QB];
+    if constexpr (kPipe) qk(0, accs[0]);
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      f32x16_t acc[QB];
+      if constexpr (kPipe) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) acc[b] = accs[sb & 1][b];
+        if (sb + 1 < NSB) qk(sb + 1, accs[(sb + 1) & 1]);
+      } else {
+        qk(sb, acc);
       }
       float sv[QB][16];
 #pragma unroll
@@ -1248,7 +1262,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
         MQ::mma(acc, fa, qf[t]);
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sv[kb][r] = (kb * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
+      for (int r = 0; r < 16; ++r) sv[kb][r] = acc[r];
+      if (kb * 32 + 32 > K) {   // wave-uniform: only the block that runs past K is masked
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kb * 32 + acc_row(r, hh) >= K) sv[kb][r] = -INFINITY;
+      }
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -1274,9 +1293,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
 
   typename MQ::frag qf[NKT];
   float sv[KB][16];
-  // dense edit (bf16 PV path, program carries the bf16 mapper tile): R = P0 . M_e on the MFMA
+  // dense edit (bf16 PV path, program carries the f16 mapper tile): R = P0 . M_e on the MFMA
   constexpr bool kDenseOk = DENSE && MP::kElemBytes == 2;  // separate instantiation: its VGPRs
-  constexpr int kDenseTile = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * 2;  // bytes of the bf16 tile
+  constexpr int kDenseTile = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * 2;  // bytes of the f16 tile
   const bool dense = kDenseOk && edit;   // the launcher picks DENSE only if every edit group is
   f32x16_t Rd[KB];
   if constexpr (kDenseOk) {
@@ -1306,24 +1325,24 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     load_q(n, qf);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) Rd[kb] = f32x16_t{};
-    // P0 = hi + lo (two bf16 parts, ~2^-16 relative): R = M^T hi + M^T lo, every mapper
-    // fragment read once for both products; one 32-key block at a time (the scheduler would
-    // otherwise hoist all 36 fragment reads: 256 VGPRs)
+    // R = M^T P0 on the f16 MFMA: the mapper weights (1, 1/2, 1/4, ...) are exact in f16 and P0 in
+    // [0, 1] rounds to 11 significant bits (|dR| <= 2^-12 R, inside the 2e-3 bar); every mapper
+    // fragment read once; one 32-key block at a time (the scheduler would otherwise hoist all 18
+    // fragment reads)
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        float lo[8];
+        short8_t ph;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) lo[r] = p0[kb][8 * s2 + r] - bf2f(f2bf(p0[kb][8 * s2 + r]));
-        const MmaBf16::frag bh = MmaBf16::pack_p(p0[kb] + 8 * s2);
-        const MmaBf16::frag bl = MmaBf16::pack_p(lo);
+        for (int r = 0; r < 8; ++r) ph[r] = (short)__builtin_bit_cast(uint16_t, (_Float16)p0[kb][8 * s2 + r]);
 #pragma unroll
         for (int dt = 0; dt < KB; ++dt) {
           const MmaBf16::frag af =
               vt_frag<P2P_PROGRAM_DENSE>(reinterpret_cast<const uint16_t*>(Ms), kb * 32, s2, dt * 32, lane);
-          MmaBf16::mma(Rd[dt], af, bh);
-          MmaBf16::mma(Rd[dt], af, bl);
+          typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+          Rd[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, af.v),
+                                                          __builtin_bit_cast(f16x8_t, ph), Rd[dt], 0, 0, 0);
         }
       }
     }
@@ -1504,12 +1523,12 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
-template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false>
+template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false, bool PIPE = false>
 static void launch_multi(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16, PIPE>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
@@ -1537,6 +1556,12 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
           break;
         case 28: launch_multi<IO, MQ, D, 128, 4, 2, kF16>(a, st); return hipGetLastError();
         case 41: launch_multi<IO, MQ, D, 64, 8, 2, kF16>(a, st); return hipGetLastError();
+#ifdef P2P_EXPERIMENTS
+        case 42: launch_multi<IO, MQ, D, 128, 8, 2, kF16, true>(a, st); return hipGetLastError();
+        case 43:
+          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st); return hipGetLastError(); }
+          break;
+#endif
         default: break;
       }
     }

@@ -44,7 +44,7 @@ struct CrossArgs {
   int store_accumulate;
   int any_store;                 // some entry stores its maps
   int edit_terms;                // some group edits through the term planes (LDS gather)
-  int edit_dense;                // some group carries the dense bf16 mapper tile
+  int edit_dense;                // some group carries the dense f16 mapper tile
   int slab;                      // launcher-filled: the launch allocates the LDS slab
   int slab_stride;               // launcher-filled
   int store_slot[P2P_MAX_BATCH];

@@ -31,7 +31,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class HipError(RuntimeError):

@@ -21,8 +21,8 @@ Blob layout (include/p2p_hip.h; COLS = 128 column stride, TMAX = 8 term planes):
     header  int32[8] = n_edits, n_cols, tmax, COLS, dense, dense_offset, 0, 0
     per edit e, at byte 32 + e * REC_BYTES:
         c_rep f32[COLS] | post f32[COLS] | term {i32 row, f32 val}[TMAX][COLS]
-    dense (when every term value is exact in bf16), at byte dense_offset:
-        bf16 [n_edits][96 source words][96 target words] -- the mapper as an MFMA operand
+    dense (when every term value is exact in f16), at byte dense_offset:
+        f16 [n_edits][96 source words][96 target words] -- the mapper as an MFMA operand
 Plane t of column w holds the t-th term of that column, (0, 0.0) past its last one; the kernel
 walks the first ``tmax`` planes for every column (a wave-uniform loop of independent loads), and
 the padding adds +0.0 after the real terms, so the sums keep the sparse order exactly.
@@ -71,7 +71,7 @@ class EditProgram:
                 for t, (r, v) in enumerate(self.terms[e][w]):
                     planes[t, w, 0] = np.uint32(np.int32(r).view(np.uint32))
                     planes[t, w, 1] = np.float32(v).view(np.uint32)
-        dense = self.dense_bf16()
+        dense = self.dense_f16()
         dense_off = HEADER_BYTES + E * REC_BYTES if dense is not None else 0
         header = np.array([E, n, tmax, PROGRAM_COLS, int(dense is not None), dense_off, 0, 0], np.int32)
         parts = [header.view(np.uint8), rec.view(np.uint8).ravel()]
@@ -79,9 +79,9 @@ class EditProgram:
             parts.append(dense.view(np.uint8).ravel())
         return np.concatenate(parts)
 
-    def dense_bf16(self) -> Optional[np.ndarray]:
-        """The mappers as bf16 [E, 96, 96] (row = source word, col = target word), or None when a
-        term value is not exactly representable in bf16 (the kernel then gathers in f32)."""
+    def dense_f16(self) -> Optional[np.ndarray]:
+        """The mappers as f16 [E, 96, 96] (row = source word, col = target word), or None when a
+        term value is not exactly representable in f16 (the kernel then gathers in f32)."""
         E, n = self.n_edits, self.n_cols
         if n > DENSE:
             return None
@@ -90,7 +90,7 @@ class EditProgram:
             for w in range(n):
                 for (r, v) in self.terms[e][w]:
                     m[e, r, w] = float(np.float32(v))
-        mb = m.to(torch.bfloat16)
+        mb = m.to(torch.float16)
         if not torch.equal(mb.float(), m):
             return None
         return mb.view(torch.int16).numpy().view(np.uint16)

@@ -170,7 +170,7 @@ def test_edits_bf16_sd_geometry(cuda, tok, edit, qscale, io_dtype):
         assert prod.fused_supported()
         prog = prod._edit_program()
         # the production edit path: every weight exact in bf16 -> the dense MFMA edit (R = P0 . M)
-        assert prog.dense_bf16() is not None
+        assert prog.dense_f16() is not None
         if edit == "refine":
             assert (prog.c_rep != 0).any()          # the c_rep * P_b term of inserted words
         if edit.startswith("reweight_"):

@@ -204,7 +204,7 @@ def test_cross_edit_paths(cuda, weight, compute, tol, geom):
     mapper[1, 7, 7], mapper[1, 7, 8] = 0.0, 1.0       # swapped columns
     mapper[1, 8, 8], mapper[1, 8, 7] = 0.0, 1.0
     prog_host = programs.replace_program(mapper)
-    assert (prog_host.dense_bf16() is not None) == (weight == 0.5)
+    assert (prog_host.dense_f16() is not None) == (weight == 0.5)
     prog = prog_host.to_device(cuda)
     alpha = torch.ones(B - 1, K, device=cuda)
     alpha[2, 10:20] = 0.0                             # word-time alpha 0: own probabilities

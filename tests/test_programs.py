@@ -146,18 +146,18 @@ def test_program_blob_layout():
     assert planes[0, 6].tolist() == [5, np.float32(0.5).view(np.int32)]
     assert planes[1, 6].tolist() == [6, np.float32(0.5).view(np.int32)]
     assert planes[1, 7].tolist() == [0, 0] and not planes[2:].any()
-    dense = torch.from_numpy(blob[dense_off:].view(np.int16).copy()).view(torch.bfloat16).float().reshape(2, 96, 96)
+    dense = torch.from_numpy(blob[dense_off:].view(np.int16).copy()).view(torch.float16).float().reshape(2, 96, 96)
     want = torch.zeros(2, 96, 96)
     want[:, :77, :77] = m
     assert torch.equal(dense, want)
 
 
-def test_program_dense_only_when_exact_in_bf16():
+def test_program_dense_only_when_exact_in_f16():
     m = torch.zeros(1, 77, 77)
     m[0, torch.arange(77), torch.arange(77)] = 1
-    m[0, 3:6, 4] = 1.0 / 3                            # 1/3 is not a bf16 value
+    m[0, 3:6, 4] = 1.0 / 3                            # 1/3 is not an f16 value
     prog = programs.replace_program(m)
-    assert prog.dense_bf16() is None
+    assert prog.dense_f16() is None
     blob = prog.blob()
     assert blob[:32].view(np.int32)[4:6].tolist() == [0, 0]
     assert blob.nbytes == 32 + programs.REC_BYTES
