@@ -1165,16 +1165,24 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
             if (kb * 32 + acc_row(r, hh) >= K) sv[kb][r] = -INFINITY;
         }
       }
-      float mx = -INFINITY;
+      // K <= (KB-1)*32 + 16 (the 77 text tokens): registers 8..15 of the last block are all masked
+      auto soft = [&](auto tail) {
+        constexpr bool kShort = decltype(tail)::value;
+        float mx = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[kb][r]);
-      mx = fmaxf(mx, other_half(mx)) * c;
+          for (int r = 0; r < 16; ++r)
+            if (!(kShort && kb == KB - 1 && r >= 8)) mx = fmaxf(mx, sv[kb][r]);
+        mx = fmaxf(mx, other_half(mx)) * c;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sv[kb][r] = fast_exp2(fmaf(sv[kb][r], c, -mx));
+          for (int r = 0; r < 16; ++r)
+            sv[kb][r] = (kShort && kb == KB - 1 && r >= 8) ? 0.f : fast_exp2(fmaf(sv[kb][r], c, -mx));
+      };
+      if (K <= (KB - 1) * 32 + 16) soft(std::true_type{});
+      else soft(std::false_type{});
       f32x16_t O[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
@@ -1252,7 +1260,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   };
   // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row (K rows past
   // K hold stale LDS: their accumulator rows are replaced by -inf, never used)
-  auto probs = [&](const typename MQ::frag (&qf)[NKT], float (&sv)[KB][16]) {
+  // kShort (K <= (KB-1)*32 + 16, e.g. the 77 text tokens): registers 8..15 of the last key block
+  // hold keys >= 80, all masked -- their exponentials, sums and scalings are skipped
+  const bool short_tail = K <= (KB - 1) * 32 + 16;
+  auto probs_t = [&](const typename MQ::frag (&qf)[NKT], float (&sv)[KB][16], auto tail) {
+    constexpr bool kShort = decltype(tail)::value;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
       f32x16_t acc = {};
@@ -1273,22 +1285,32 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[kb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;
+      for (int r = 0; r < 16; ++r)
+        if (!(kShort && kb == KB - 1 && r >= 8)) mx = fmaxf(mx, sv[kb][r]);
+    mx = fmaxf(mx, other_half(mx)) * c;
     float ls = 0.f;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float ex = fast_exp2(fmaf(sv[kb][r], c, -mx));
-        sv[kb][r] = ex;
-        ls += ex;
+        if (kShort && kb == KB - 1 && r >= 8) {
+          sv[kb][r] = 0.f;
+        } else {
+          const float ex = fast_exp2(fmaf(sv[kb][r], c, -mx));
+          sv[kb][r] = ex;
+          ls += ex;
+        }
       }
-    const float inv = 1.f / (ls + __shfl_xor(ls, 32));
+    const float inv = 1.f / (ls + other_half(ls));
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sv[kb][r] *= inv;
+      for (int r = 0; r < 16; ++r)
+        if (!(kShort && kb == KB - 1 && r >= 8)) sv[kb][r] *= inv;
+  };
+  auto probs = [&](const typename MQ::frag (&qf)[NKT], float (&sv)[KB][16]) {
+    if (short_tail) probs_t(qf, sv, std::true_type{});
+    else probs_t(qf, sv, std::false_type{});
   };
 
   typename MQ::frag qf[NKT];
@@ -1311,11 +1333,13 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
                                                        (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES);
       const float* al = a.grp_alpha[gi] + (b - 1) * K;
+      // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B: two coefficients per column
       float* col = reinterpret_cast<float*>(cross_dyn + kDenseTile);
       for (int w = tid; w < KR; w += NT) {
-        col[w] = ce[w];
-        col[KR + w] = ce[P2P_PROGRAM_COLS + w];
-        col[2 * KR + w] = w < K ? al[w] : 0.f;
+        const float aw = w < K ? al[w] : 0.f;
+        const float ap = aw * ce[P2P_PROGRAM_COLS + w];
+        col[w] = fmaf(ap, ce[w], 1.f - aw);
+        col[KR + w] = ap;
       }
     }
     stage(first, false);
@@ -1372,7 +1396,6 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   probs(qf, sv);
 
   if (dense) {
-#pragma clang fp contract(off)
     // a lane's columns come in runs of 4 (r & 3): one 16-byte LDS read per run and table;
     // one 32-column block at a time (hoisting every read costs ~150 VGPRs)
     const float* const col = reinterpret_cast<const float*>(cross_dyn + kDenseTile);
@@ -1381,15 +1404,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int w0 = kb * 32 + 8 * g + 4 * hh;
-        const f32x4_t c4 = *reinterpret_cast<const f32x4_t*>(col + w0);
-        const f32x4_t p4 = *reinterpret_cast<const f32x4_t*>(col + KR + w0);
-        const f32x4_t a4 = *reinterpret_cast<const f32x4_t*>(col + 2 * KR + w0);
+        const f32x4_t A4 = *reinterpret_cast<const f32x4_t*>(col + w0);
+        const f32x4_t B4 = *reinterpret_cast<const f32x4_t*>(col + KR + w0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g + j;
-          const float pb = sv[kb][r];
-          const float R = p4[j] * (c4[j] * pb + Rd[kb][r]);
-          sv[kb][r] = a4[j] * R + (1.f - a4[j]) * pb;   // columns >= K: a = 0, p stays 0
+          sv[kb][r] = fmaf(sv[kb][r], A4[j], Rd[kb][r] * B4[j]);   // columns >= K: A = 1, B = 0
         }
       }
     }
@@ -1608,7 +1628,7 @@ static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
   b.slab = (a.any_store || ((a.edit_terms || a.edit_dense) && !dense)) ? 1 : 0;
   size_t dyn = b.slab ? (size_t)W * 32 * b.slab_stride * sizeof(float) : 0;
   const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t) +
-                      3 * P2P_MAX_KEYS_CROSS * sizeof(float);
+                      2 * P2P_MAX_KEYS_CROSS * sizeof(float);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
   if (dense)

@@ -63,6 +63,39 @@ def test_null_text_inversion_matches_oracle(cuda, use_graphs):
         assert cos(d_prod, d_want) >= 0.95
 
 
+def test_null_text_inversion_full_schedule(cuda):
+    """configs[4] at its stated schedule: 50 DDIM steps x 10 Adam steps (null_text.py:591-618,
+    early stop 1e-5), graphed product path vs the oracle's fp32 autograd on the same weights.  Over
+    50 dependent steps the bf16-kernel gradients drift, so the per-step bar is on the optimiser's
+    updates (cosine >= 0.9) and on the embeddings themselves (>= 0.999); the DDIM trajectory is a
+    forward-only quantity and stays at >= 0.9999."""
+    steps, inner = 50, 10
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.randn(1, 4, 64, 64, generator=g).to(cuda)
+    with config.compute_mode("bf16"):
+        inv = null_text.NullInversion(model, num_ddim_steps=steps, use_graphs=True)
+        (_, _), x_T, embs = inv.invert(x0, PROMPT, num_inner_steps=inner, early_stop_epsilon=1e-5)
+        prod_traj = inv.ddim_loop(x0)
+    ofw.install(model, None)
+    sched = model.scheduler
+    sched.set_timesteps(steps)
+    uncond, cond = inv.context.chunk(2)
+    ac, fa = sched.alphas_cumprod.to(cuda), sched.final_alpha_cumprod.to(cuda)
+    traj = ont.ddim_loop(model.unet, ac, fa, sched.timesteps, cond, x0, steps)
+    want_embs, _ = ont.null_optimization(model.unet, ac, fa, sched.timesteps, uncond, cond, traj, steps, inner, 1e-5)
+    assert min(cos(a, b) for a, b in zip(prod_traj, traj)) >= 0.9999
+    u0 = uncond[:1]
+    worst_e, worst_u = 1.0, 1.0
+    for i, (e, w) in enumerate(zip(embs, want_embs)):
+        worst_e = min(worst_e, cos(e, w))
+        if (w - u0).norm().item() > 1e-6:
+            worst_u = min(worst_u, cos(e - u0, w - u0))
+    print(f"50x10 null-text: worst cos(embeddings) {worst_e:.6f}, worst cos(updates) {worst_u:.4f}")
+    assert worst_e >= 0.999
+    assert worst_u >= 0.9
+
+
 def test_edit_with_null_embeddings(cuda, tok):
     """The P2P edit after inversion: per-step null embeddings + fused AttentionReplace."""
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
