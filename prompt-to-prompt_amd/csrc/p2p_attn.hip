@@ -1613,9 +1613,8 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename IO, typename MQ, typename MP, int D>
-static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
-  constexpr int W = (MP::kElemBytes == 4 && D >= 128) ? 2 : 4;
+template <typename IO, typename MQ, typename MP, int D, int W>
+static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   CrossArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   // the slab holds a [32, K] f32 block per wave: stride K | 1 (odd, so the 32 rows of one
@@ -1636,6 +1635,16 @@ static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false>), grid, block, dyn, st, b);
   return hipGetLastError();
+}
+
+template <typename IO, typename MQ, typename MP, int D>
+static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
+#ifdef P2P_EXPERIMENTS
+  // 50: two-wave workgroups (twice the workgroups) for the small bf16 grids (d <= 80)
+  if constexpr (MP::kElemBytes == 2 && D <= 80)
+    if (a.variant == 50) return launch_cross_w<IO, MQ, MP, D, 2>(a, st);
+#endif
+  return launch_cross_w<IO, MQ, MP, D, (MP::kElemBytes == 4 && D >= 128) ? 2 : 4>(a, st);
 }
 
 #define P2P_FOR_EACH_D(X) X(8) X(16) X(32) X(40) X(64) X(80) X(128) X(160)

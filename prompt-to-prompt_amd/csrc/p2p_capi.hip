@@ -121,6 +121,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
   if (t->n_key > P2P_MAX_KEYS_CROSS) return P2P_E_KEYS;
   if (!groups || n_groups < 1 || n_groups > P2P_MAX_GROUPS) return P2P_E_BATCH;
   CrossArgs a;
+  a.variant = self_variant();
   fill_common(a, t);
   int covered = 0;
   for (int n = 0; n < t->n_batch; ++n) a.ent_group[n] = -1;

@@ -47,6 +47,7 @@ struct CrossArgs {
   int edit_dense;                // some group carries the dense f16 mapper tile
   int slab;                      // launcher-filled: the launch allocates the LDS slab
   int slab_stride;               // launcher-filled
+  int variant;                   // launch-shape experiments (P2P_SELF_VARIANT, experiments build only)
   int store_slot[P2P_MAX_BATCH];
   int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
   int grp_first[P2P_MAX_GROUPS];

@@ -4,7 +4,8 @@ config-2 U-Net call (N = 8 = 4 uncond + 4 cond, H = 8, K = 77, bf16 IO):
   edit        : north-star AttentionReplace program on the cond group
   store       : no edit, cond-half maps accumulated into the store
   edit+store  : both (what G2/G3/G5/G6 run every step)
-Usage: python tools/cross_bench.py [iters]"""
+Usage: [CROSS_BENCH_GRAPH=1] python tools/cross_bench.py [iters]   (graph mode: GPU time without the
+host enqueue, which otherwise floors every launch at ~11 us)"""
 import json
 import os
 import sys
@@ -31,6 +32,33 @@ def time_fn(fn, iters, warm=5):
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1e3
+
+
+def time_graph(fn, iters, reps=5):
+    """GPU time per launch without the Python + ctypes enqueue: `iters` launches captured in one
+    HIP graph, replayed `reps` times."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (reps * iters) * 1e3
+
+
+TIMER = time_graph if os.environ.get("CROSS_BENCH_GRAPH") == "1" else time_fn
 
 
 def main(iters=50):
@@ -61,7 +89,7 @@ def main(iters=50):
             fn = lambda: _hip.cross_attn(q, k, v, o, H, d ** -0.5, grp, store=st,  # noqa: E731
                                          store_slot=slots if st is not None else None,
                                          accumulate=st is not None)
-            r[tag + "_us"] = round(time_fn(fn, iters), 2)
+            r[tag + "_us"] = round(TIMER(fn, iters), 2)
         print(json.dumps(r), flush=True)
         rows.append(r)
     return rows
