@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 out=gpurun_out/${1:-r02ev}
 mkdir -p $out
 echo "== gpu tests"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $out/gpu_tests.log 2>&1; rc=$?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 400 --timeout-method thread > $out/gpu_tests.log 2>&1; rc=$?
 tail -3 $out/gpu_tests.log; echo "tests rc=$rc"; [ $rc -ne 0 ] && exit $rc
 echo "== smoke"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1; rc=$?
