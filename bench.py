@@ -216,7 +216,11 @@ def main():
     torch.cuda.synchronize(dev)
     timer.enabled = True
     t0 = time.perf_counter()
-    outs = [batch(b) for b in timed]
+    outs = []
+    for i, b in enumerate(timed):
+        outs.append(batch(b))
+        if len(timed) > 4:   # long sweeps: a progress line per batch (stderr; host-side only)
+            print(f"[bench rank {rank}] batch {i + 1}/{len(timed)}", file=sys.stderr, flush=True)
     lats = torch.cat([o[0] for o in outs]).float() if outs else torch.zeros(0, B, 4, 64, 64, device=dev)
     maps = torch.cat([o[1] for o in outs]).float() if outs else torch.zeros(0, B, 16, 16, 77, device=dev)
     # ONE RCCL all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
@@ -245,7 +249,7 @@ def main():
                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "algorithmic_bytes": 4.0 * 8 * G * 4096 * 320 * 2,
-                    "kernel": f"self_attn_multi_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 2 x 32 queries per wave, 128-key tiles)",
+                    "kernel": f"self_attn_multi_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 2 x 32 queries per wave, 256-key tiles, pipelined sub-blocks)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
         cpu = None

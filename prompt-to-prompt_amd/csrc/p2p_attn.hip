@@ -1564,12 +1564,16 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
       constexpr bool kF16 = MQ::planes == 1 && sizeof(IO) == 2;
       if (a.variant == 0 && a.P >= 2048) {
-        // bf16 inputs: the F16 form (scale and reference point inside the MFMA)
-        launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st);
+        // bf16 inputs: the F16 form (scale and reference point inside the MFMA) with 256-key tiles
+        // and sub-block-pipelined Q K^T (G1: 0.2094 -> 0.2066 ms, profiles/r02/g1_ab/r02t_pipe256.log);
+        // the split-bf16 path (two K planes) keeps 128-key tiles (LDS)
+        if constexpr (MQ::planes == 1) launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st);
+        else launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st);
         return hipGetLastError();
       }
       switch (a.variant) {
         case 40: launch_multi<IO, MQ, D, 128, 8, 2>(a, st); return hipGetLastError();
+        case 44: launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st); return hipGetLastError();
         case 17: launch_multi<IO, MQ, D, 64, 4, 2, kF16>(a, st); return hipGetLastError();
         case 27:
           if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16>(a, st); return hipGetLastError(); }

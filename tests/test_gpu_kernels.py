@@ -116,13 +116,13 @@ def test_bf16_inputs_exact_products(cuda):
     assert (store - p).abs().max().item() < 2e-3
 
 
-@pytest.mark.parametrize("case", ["plain", "peaky32", "k_past_f16", "q_past_f16", "remap"])
+@pytest.mark.parametrize("case", ["plain", "peaky32", "k_past_f16", "q_past_f16", "remap", "ragged"])
 def test_self_attention_f16_form(cuda, case):
     """The d = 40 production form (bf16 inputs, P >= 2048): Q prescaled by scale*log2(e) in f16, K
     staged as f16, -m in Q's padding column.  Within the bf16 O bound on peaky rows; inputs past
     the f16 range (|k| >= 65520, |c q| >= 65520) take the exact bf16 recompute and stay exact."""
-    N, P, K, H, d = 2, 2048, 2048, 2, 40
-    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=31)
+    N, P, K, H, d = (2, 2100, 2100, 2, 40) if case == "ragged" else (2, 2048, 2048, 2, 40)   # ragged: a partial
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=31)  # key tile
     if case == "k_past_f16":
         k[1, 100, 3] = 70000.0          # one key element of entry 1, head 0
         q[1, :, 3] = 1e-3               # keeps its logits finite and moderate
