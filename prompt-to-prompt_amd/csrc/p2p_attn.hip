@@ -446,7 +446,8 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_fused_kernel(SelfArgs a)
 //   * values outside the f16 range (|k| >= 65520, |c q| >= 65520, |m| >= 65504) set a flag and
 //     the workgroup recomputes on the exact bf16 path (K restaged as bf16, fma with c), like the
 //     NOMAX overflow recompute.
-template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool F16 = false, bool PIPE = false>
+template <typename IO, typename MQ, int D, int BK, int WAVES, int QB, bool F16 = false, bool PIPE = false,
+          bool PRIO = false>
 __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a) {
   using EK = typename MQ::elem;
   constexpr int DK = (D + 15) / 16 * 16;
@@ -624,6 +625,9 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
   stage_write(0, std::false_type{});
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
+  // PRIO (experiment): static priority 1 for the second-dispatched half of the waves
+  if constexpr (PRIO)
+    if (wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   bool bad = false;
   // One tile, sub-block by sub-block (Q K^T, [max decision], exp, P V): only one sub-block's scores
   // per query block are live.  Slow tiles (the first one, and the overflow recompute) move the
@@ -1543,12 +1547,13 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
-template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false, bool PIPE = false>
+template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false, bool PIPE = false,
+          bool PRIO = false>
 static void launch_multi(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16, PIPE>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16, PIPE, PRIO>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
@@ -1584,6 +1589,9 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
         case 42: launch_multi<IO, MQ, D, 128, 8, 2, kF16, true>(a, st); return hipGetLastError();
         case 43:
           if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st); return hipGetLastError(); }
+          break;
+        case 45:
+          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true, true>(a, st); return hipGetLastError(); }
           break;
 #endif
         default: break;
