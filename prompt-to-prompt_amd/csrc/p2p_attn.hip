@@ -19,15 +19,6 @@
 
 namespace p2p {
 
-// The value held by lane l ^ 32 (the other half of the wave), via v_permlane32_swap: no LDS
-// round trip (ds_bpermute) on the softmax critical path.
-__device__ __forceinline__ float other_half(float x) {
-  const unsigned u = __float_as_uint(x);
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  // r[0]: lanes 0-31 keep x, lanes 32-63 get the low half's x; r[1]: the high half's x everywhere
-  return (threadIdx.x & 32) ? __uint_as_float(r[0]) : __uint_as_float(r[1]);
-}
-
 template <typename E>
 __device__ __forceinline__ E one_elem();
 template <>
@@ -1539,7 +1530,12 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
   else if constexpr (kOnes && MP::kElemBytes == 2) {
     // O only (no lse): no per-tile max (P2P_SELF_VARIANT 16 in an experiments build keeps it)
-    if (a.lse == nullptr && a.variant != 16 && a.variant != 30)
+#ifdef P2P_EXPERIMENTS
+    if (a.lse == nullptr && a.variant == 16)
+      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+    else
+#endif
+    if (a.lse == nullptr)
       hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false, true>), grid, block, 0, st, b);
     else
       hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
@@ -1560,22 +1556,25 @@ template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int BK = (D >= 128 || MP::kElemBytes == 4) ? 32 : 64;
   if constexpr (MP::kElemBytes == 2 && D == 40) {
-    // d = 40 on the bf16 pipe, nothing but O wanted (G1/G7 without kept maps or autograd):
-    // two 32-row query blocks per wave, 128-key tiles, 8-wave workgroups -- 512 queries per
-    // workgroup, so only where that still fills the grid (P >= 2048).  Experiments build
-    // (P2P_SELF_VARIANT): 40 = the bf16 form (v_fma per score), 16 = the 64-key kernel with the
-    // per-tile max, 29 = the same without (NOMAX), 27 = 256-key tiles, 28 = 4-wave workgroups,
-    // 17 = 64-key tiles x 4 waves.
+    // d = 40 on the bf16 pipe, nothing but O wanted (G1/G7 without kept maps or autograd)
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
       constexpr bool kF16 = MQ::planes == 1 && sizeof(IO) == 2;
+      // bf16 inputs: the software-pipelined F16-form kernel (p2p_self40.hip); experiments
+      // variants 40-45 select the round-2 multi-block kernel instead
+      if constexpr (kF16)
+        if (self40_eligible(a) && (a.variant == 0 || a.variant >= 60)) return (hipError_t)run_self40(a, st);
       if (a.variant == 0 && a.P >= 2048) {
-        // bf16 inputs: the F16 form (scale and reference point inside the MFMA) with 256-key tiles
-        // and sub-block-pipelined Q K^T (G1: 0.2094 -> 0.2066 ms, profiles/r02/g1_ab/r02t_pipe256.log);
-        // the split-bf16 path (two K planes) keeps 128-key tiles (LDS)
+        // f32 inputs (split-bf16 Q K^T, two K planes): the multi-block kernel, 128-key tiles;
+        // bf16 inputs with K < 256: the same with the F16 form
         if constexpr (MQ::planes == 1) launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st);
         else launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st);
         return hipGetLastError();
       }
+#ifdef P2P_EXPERIMENTS
+      // A/B timing of the round-2 shapes: 40 = the bf16 form (v_fma per score), 44 = F16 form,
+      // 128-key tiles, 17 = 64-key tiles x 4 waves, 27 = 256-key tiles, 28 = 4-wave workgroups,
+      // 41 = 64-key tiles x 8 waves, 42/43 = sub-block-pipelined Q K^T (128/256-key tiles),
+      // 45 = 43 with static priority for waves 4-7
       switch (a.variant) {
         case 40: launch_multi<IO, MQ, D, 128, 8, 2>(a, st); return hipGetLastError();
         case 44: launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st); return hipGetLastError();
@@ -1585,7 +1584,6 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
           break;
         case 28: launch_multi<IO, MQ, D, 128, 4, 2, kF16>(a, st); return hipGetLastError();
         case 41: launch_multi<IO, MQ, D, 64, 8, 2, kF16>(a, st); return hipGetLastError();
-#ifdef P2P_EXPERIMENTS
         case 42: launch_multi<IO, MQ, D, 128, 8, 2, kF16, true>(a, st); return hipGetLastError();
         case 43:
           if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st); return hipGetLastError(); }
@@ -1593,9 +1591,9 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
         case 45:
           if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true, true>(a, st); return hipGetLastError(); }
           break;
-#endif
         default: break;
       }
+#endif
     }
   }
   if (mode == MODE_FUSED) {
@@ -1604,12 +1602,16 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
       if (a.P > 64) {
         // default: 8 waves x 32 query rows per workgroup, 64-key tiles (measured best at
         // d = 40 and within 2 % of best at d = 80: tools/attn_bench.py, profiles/)
+#ifdef P2P_EXPERIMENTS
         switch (a.variant) {
           case 1: launch_fused<IO, MQ, MP, D, 64, 4>(a, st); return hipGetLastError();
           case 2: launch_fused<IO, MQ, MP, D, 128, 4>(a, st); return hipGetLastError();
           case 3: launch_fused<IO, MQ, MP, D, 128, 8>(a, st); return hipGetLastError();
-          default: launch_fused<IO, MQ, MP, D, 64, 8>(a, st); return hipGetLastError();
+          default: break;
         }
+#endif
+        launch_fused<IO, MQ, MP, D, 64, 8>(a, st);
+        return hipGetLastError();
       }
     }
     if (a.P <= 64) launch_fused<IO, MQ, MP, D, BK, 2>(a, st);
@@ -1682,11 +1684,14 @@ static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
   dim3 grid(n_kgroups * b.n_qtiles * a.H * a.n_maps), block(256);
   // non-temporal running-sum accesses (the map streams through once per step: -7.5 % at G2 with
   // the maps HBM-resident; two key blocks per step measured +2 %, not instantiated).
-  // P2P_SELF_VARIANT=6 keeps plain accesses for A/B timing.
-  if (a.variant == 6)
+  // P2P_SELF_VARIANT=6 (experiments build) keeps plain accesses for A/B timing.
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 6) {
     hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, false>), grid, block, 0, st, b, kw, n_kgroups);
-  else
-    hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
   return hipGetLastError();
 }
 
@@ -1697,11 +1702,14 @@ static hipError_t launch_self_probs_d(const SelfArgs& a, hipStream_t st) {
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(b.n_qtiles * a.H * a.N), block(256);
   // non-temporal probability stores (a write-once stream: G1 1.33 -> 1.04 ms, G2 118 -> 104 us);
-  // P2P_SELF_VARIANT=7 keeps plain stores for A/B timing
-  if (a.variant == 7)
+  // P2P_SELF_VARIANT=7 (experiments build) keeps plain stores for A/B timing
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 7) {
     hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, false>), grid, block, 0, st, b, kw);
-  else
-    hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, true>), grid, block, 0, st, b, kw);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, true>), grid, block, 0, st, b, kw);
   return hipGetLastError();
 }
 

@@ -348,6 +348,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// The value held by lane l ^ 32 (the other half of the wave), via v_permlane32_swap: no LDS
+// round trip (ds_bpermute) on the softmax critical path.
+__device__ __forceinline__ float other_half(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  // r[0]: lanes 0-31 keep x, lanes 32-63 get the low half's x; r[1]: the high half's x everywhere
+  return (threadIdx.x & 32) ? __uint_as_float(r[0]) : __uint_as_float(r[1]);
+}
+
 // Row stride (in elements) of an LDS tile read with ds_read_b128 by 16 distinct rows at the
 // same column: a byte stride of 16 * odd spreads any 16 consecutive rows over all 16 slots.
 template <int D, int ES>

@@ -1,0 +1,464 @@
+// d = 40 self-attention, O only: the G1/G7 layers of the SD-v1.4 U-Net (P = K = 4096, 8 heads)
+// without kept maps or autograd -- the dominant kernel of the hot path (ptp_utils.py:195-206).
+//
+// Round-3 form: software-pipelined over 32x32 blocks.  A wave owns QB 32-row query blocks; the
+// blocks of a tile are walked in the order x = (32-key sub-block, query block), and step x issues
+//     Q K^T of block x+1 (3 MFMAs)  |  exp2 + bf16 pack of block x (16 v_exp, 8 v_cvt_pk)  |  P V of block x-1 (4 MFMAs)
+// so every MFMA has exponentials of an independent block beside it and every exponential an
+// MFMA: the wave's own instruction stream interleaves the matrix pipe and the VALU instead of
+// relying on a co-resident wave to fill the gaps (MI355X_MICROARCH.md, "one wave per SIMD").
+// K/V fragments for sub-block sb+1 are read from LDS while sub-block sb computes (double-
+// buffered fragments), and the next tile's K/V are staged into the other LDS buffer by
+// register staging spread over the second half of the tile.
+//
+// Arithmetic (the F16 form of round 2, kept): Q is prescaled by c = scale*log2(e) and rounded
+// to f16; K is staged as f16 (exact for bf16 values in range); d pads to 48 and the padding
+// column carries the reference point (K[:,40] = 1, Q[:,40] = -m), so S^T = c s - m leaves the
+// MFMA and p = exp2(S^T) costs one v_exp.  V's column 40 is 1, so O^T row 40 is the row sum of
+// the same bf16 p that P V uses.  The reference point m of a query row is the maximum over the
+// first 32 keys (no per-tile maximum); a tile whose row sum passes 2^64 moves m up by 64 and
+// rescales O by the exact factor.  Anything outside the fast form's range -- |c q| or |k| past
+// the f16 range, |m| >= 65504, a non-finite row sum -- flags the workgroup, which recomputes
+// everything on the exact bf16 path (unscaled bf16 Q and K, running max per sub-block).
+#include <type_traits>
+#include <utility>
+
+#include "p2p_device.h"
+#include "p2p_kernels.h"
+
+namespace p2p {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+
+constexpr int kD = 40;
+constexpr int kNKT = 3;    // 16-deep k steps of Q K^T (d padded to 48)
+constexpr int kNDT = 2;    // 32-row tiles of O^T (d padded to 64: rows 0-39 data, 40 row sums)
+constexpr int kKS = 56;    // f16 elements per K row in LDS: 112 B, a b128 read of 16 rows hits 16 slots
+constexpr int kVS = 96;    // bf16 elements per V row in LDS: 192 B, conflict-free transposed reads
+constexpr int kCPR = kD / 8;   // 16-byte chunks per K/V row
+
+template <int... I, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+__device__ __forceinline__ short8_t lds_b128(const uint16_t* p) { return *reinterpret_cast<const short8_t*>(p); }
+
+__device__ __forceinline__ void mma_f16(f32x16_t& acc, const short8_t& k, const short8_t& q) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, k), __builtin_bit_cast(f16x8_t, q), acc,
+                                               0, 0, 0);
+}
+__device__ __forceinline__ void mma_bf16(f32x16_t& acc, const short8_t& a, const short8_t& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), acc,
+                                                0, 0, 0);
+}
+
+// One workgroup = WAVES waves x QB query blocks of 32 rows = 32*QB*WAVES queries of one (entry,
+// head); BK-key tiles, double-buffered in LDS.
+template <int WAVES, int QB, int BK, bool SCHED>
+__global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(SelfArgs a) {
+  constexpr int NSB = BK / 32;
+  constexpr int NT = 64 * WAVES;
+  constexpr int NCH = (BK * kCPR + NT - 1) / NT;
+  constexpr int KBUF = BK * kKS;
+  constexpr int VBUF = BK * kVS;
+  constexpr int X = NSB * QB;   // pipeline steps (32x32 blocks) per tile
+  constexpr float kThr = 8.0f;  // exact path: defer-max threshold (log2 units)
+  constexpr int kHalf = X / 2;  // staging writes start here, one chunk every kSpread steps
+  constexpr int kSpread = (X - kHalf) / NCH > 0 ? (X - kHalf) / NCH : 1;
+  static_assert(kHalf + (NCH - 1) * kSpread < X, "every staged chunk is written inside the tile");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2 * KBUF];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2 * VBUF];
+  __shared__ int wg_flag;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qi = lane & 31;
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H;
+  const int n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int pw = (qt * WAVES + wave) * 32 * QB;   // first query of this wave
+  const int K = a.K;
+  const float c = a.scale_log2;
+
+  const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * kD;
+  const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * kD;
+  const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * kD;
+
+  // padding columns (written once; staging writes columns 0-39 only): K col 40 = f16 1.0 (the
+  // -m column), 41-47 = 0; V col 40 = bf16 1.0 (row sums), 41-63 = 0
+  for (int r = tid; r < 2 * BK; r += NT) {
+    *reinterpret_cast<short8_t*>(Ks + r * kKS + kD) = short8_t{0x3C00, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      *reinterpret_cast<short8_t*>(Vs + r * kVS + kD + 8 * j) =
+          short8_t{(short)(j == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
+  }
+  if (tid == 0) wg_flag = 0;
+
+  // ---- Q fragments: lane (qi, hh) of block b, k step t holds Q[p][16t + 8hh .. +7]
+  bool ovf = false;
+  short8_t qf[QB][kNKT];
+  auto load_q = [&](bool prescale) __attribute__((always_inline)) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int t = 0; t < kNKT; ++t) {
+        const int col = 16 * t + 8 * hh;
+        const int p = pw + 32 * b + qi;
+        short8_t v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        if (p < a.P && col < kD) v = *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + col);
+        if (prescale) {
+          float mx = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float x = bf2f((uint16_t)v[j]) * c;
+            mx = fmaxf(mx, fabsf(x));
+            v[j] = (short)__builtin_bit_cast(uint16_t, (_Float16)x);
+          }
+          ovf |= !(mx < 65520.f);
+        }
+        qf[b][t] = v;
+      }
+  };
+  load_q(true);
+  // Q column 40 (k step 2, lane half 1, element 0) holds -m
+  auto set_mcol = [&](int b, float m) __attribute__((always_inline)) {
+    if (hh == 1) qf[b][2][0] = (short)__builtin_bit_cast(uint16_t, (_Float16)(-m));
+  };
+
+  // ---- K/V staging: chunk i of this thread = row cidx / 5, 16-byte chunk cidx % 5
+  short8_t kreg[NCH], vreg[NCH];
+  uint32_t koff[NCH], voff[NCH];
+  int lrow[NCH], lch[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int cidx = tid + i * NT;
+    const int row = min(cidx / kCPR, BK - 1);
+    const int ch = cidx - (cidx / kCPR) * kCPR;
+    lrow[i] = row;
+    lch[i] = ch;
+    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * 2);
+    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
+  }
+  const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + kD) * 2;
+  const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + kD) * 2;
+  const int64_t kstep = (int64_t)BK * a.ldk * 2;
+  const int64_t vstep = (int64_t)BK * a.ldv * 2;
+  auto chunk_live = [&](int i) __attribute__((always_inline)) {
+    return (BK * kCPR) % NT == 0 || tid + i * NT < BK * kCPR;
+  };
+  auto stage_load = [&](int kt) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (chunk_live(i)) {
+        kreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)koff[i], 0, 0));
+        vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)voff[i], 0, 0));
+      }
+  };
+  // chunk i into LDS buffer buf: K as f16 (fast form; exact inside the f16 range, RTZ packing
+  // would clamp past 65504 silently, so the range is checked) or raw bf16 (exact path)
+  auto stage_write = [&](int i, int buf, bool as_f16) __attribute__((always_inline)) {
+    if (!chunk_live(i)) return;
+    uint16_t* const kd = Ks + buf * KBUF + lrow[i] * kKS + lch[i] * 8;
+    if (as_f16) {
+      short8_t hv;
+      float mx = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float x0 = bf2f((uint16_t)kreg[i][j]), x1 = bf2f((uint16_t)kreg[i][j + 1]);
+        mx = fmaxf(mx, fmaxf(fabsf(x0), fabsf(x1)));
+        const auto pk = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x0, x1));
+        hv[j] = (short)(pk & 0xffff);
+        hv[j + 1] = (short)(pk >> 16);
+      }
+      ovf |= !(mx < 65504.f);
+      *reinterpret_cast<short8_t*>(kd) = hv;
+    } else {
+      *reinterpret_cast<short8_t*>(kd) = kreg[i];
+    }
+    *reinterpret_cast<short8_t*>(Vs + buf * VBUF + lrow[i] * kVS + lch[i] * 8) = vreg[i];
+  };
+
+  const int ntiles = (K + BK - 1) / BK;
+  const int nfull = K / BK;
+  f32x16_t O[QB][kNDT];
+  float m_ref[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b)
+#pragma unroll
+    for (int dt = 0; dt < kNDT; ++dt) O[b][dt] = f32x16_t{};
+
+  // LDS fragment reads: K^T operand of sub-block sb (3 k steps), V^T operand (2 k steps x 2 d tiles)
+  auto read_k = [&](const uint16_t* Kb, int sb, short8_t (&kf)[kNKT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < kNKT; ++t) kf[t] = lds_b128(Kb + (sb * 32 + qi) * kKS + 16 * t + 8 * hh);
+  };
+  auto read_v = [&](const uint16_t* Vb, int sb, short8_t (&vf)[2][kNDT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < kNDT; ++dt) vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
+  };
+
+  stage_load(0);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) stage_write(i, 0, true);
+  __syncthreads();
+
+  // ---- reference point: the row maximum of c s over the first 32 keys (Q column 40 is still 0)
+  {
+    short8_t kf[kNKT];
+    read_k(Ks, 0, kf);
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      f32x16_t acc = f32x16_t{};
+#pragma unroll
+      for (int t = 0; t < kNKT; ++t) mma_f16(acc, kf[t], qf[b][t]);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+      mx = fmaxf(mx, other_half(mx));
+      const float m = (float)(_Float16)mx;   // representable in Q's f16 column
+      ovf |= !(fabsf(m) < 65504.f);
+      m_ref[b] = m;
+      set_mcol(b, m);
+    }
+  }
+
+  bool bad = false;
+  // ---- one tile of the fast form, software-pipelined over its X blocks.  more: the next tile
+  // is staged during this one (compile-time, so the tile body is one basic block); masked: keys
+  // past K in this tile
+  auto tile = [&](int kt, auto more, auto masked) __attribute__((always_inline)) {
+    constexpr bool kMore = decltype(more)::value;
+    constexpr bool kMasked = decltype(masked)::value;
+    const int buf = kt & 1;
+    if constexpr (kMore) stage_load(kt + 1);
+    const uint16_t* const Kb = Ks + buf * KBUF;
+    const uint16_t* const Vb = Vs + buf * VBUF;
+    short8_t kf[2][kNKT];
+    short8_t vf[2][2][kNDT];
+    f32x16_t S[2];
+    short8_t pf[2][2];
+    read_k(Kb, 0, kf[0]);
+    read_v(Vb, 0, vf[0]);
+    auto qk = [&](int x) __attribute__((always_inline)) {
+      const int sb = x / QB, b = x % QB;
+      S[x & 1] = f32x16_t{};
+#pragma unroll
+      for (int t = 0; t < kNKT; ++t) mma_f16(S[x & 1], kf[sb & 1][t], qf[b][t]);
+    };
+    auto pv = [&](int x) __attribute__((always_inline)) {
+      const int sb = x / QB, b = x % QB;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < kNDT; ++dt) mma_bf16(O[b][dt], vf[sb & 1][s2][dt], pf[x & 1][s2]);
+    };
+    auto ex = [&](int x) __attribute__((always_inline)) {
+      const int sb = x / QB;
+      float e[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float s = S[x & 1][r];
+        if constexpr (kMasked)
+          if (kt * BK + sb * 32 + acc_row(r, hh) >= K) s = -INFINITY;
+        e[r] = fast_exp2(s);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[x & 1][s2][j] = (short)f2bf(e[8 * s2 + j]);
+    };
+    qk(0);
+    if constexpr (SCHED) __builtin_amdgcn_sched_barrier(0);
+    static_for<X>([&](auto xc) __attribute__((always_inline)) {
+      constexpr int x = decltype(xc)::value;
+      constexpr int sb = x / QB, b = x % QB;
+      constexpr bool kRdK = b == 0 && sb + 1 < NSB;
+      constexpr bool kRdV = b == (QB > 1 ? 1 : 0) && sb + 1 < NSB;
+      // the next tile's chunks go to the other buffer over the second half of the tile (every
+      // wave has passed the barrier that ended the tile which last read that buffer)
+      constexpr bool kStw = kMore && x >= kHalf && (x - kHalf) % kSpread == 0 && (x - kHalf) / kSpread < NCH;
+      if constexpr (kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
+      if constexpr (kRdV) read_v(Vb, sb + 1, vf[(sb + 1) & 1]);
+      if constexpr (x + 1 < X) qk(x + 1);
+      ex(x);
+      if constexpr (x >= 1) pv(x - 1);
+      if constexpr (kStw) stage_write((x - kHalf) / kSpread, buf ^ 1, true);
+      if constexpr (SCHED) {
+        // one MFMA per slot, the step's VALU spread evenly over the slots, LDS reads early
+        // (masks: MFMA 0x8, VALU 0x2 -- which excludes the transcendental v_exp --, TRANS
+        // 0x400, DS_READ 0x100, DS_WRITE 0x200)
+        constexpr int nm = (x + 1 < X ? kNKT : 0) + (x >= 1 ? 2 * kNDT : 0);
+        constexpr int ne = 16;
+        constexpr int nv = 8 + (kStw ? 24 : 0) + (kMasked ? 32 : 0);
+        constexpr int nr = (kRdK ? kNKT : 0) + (kRdV ? 8 : 0);
+        static_for<nm>([&](auto ic) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value;
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x400, (ne * (i + 1)) / nm - (ne * i) / nm, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, (nv * (i + 1)) / nm - (nv * i) / nm, 0);
+          if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, (nr * (i + 1)) / nm - (nr * i) / nm, 0);
+          if constexpr (kStw && i < 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    pv(X - 1);
+    // row sums (O^T row 40 = d tile 1, register 4 of the low lane half): a sum past 2^64 moves
+    // the reference point up by 64 (rounded to f16) and rescales O by the exact factor
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      const float own = O[b][1][4];
+      const float lsum = own + other_half(own);
+      bad |= !(lsum < INFINITY);
+      if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
+        if (lsum > 0x1p64f) {
+          const float mnew = (float)(_Float16)(m_ref[b] + 64.f);
+          ovf |= !(fabsf(mnew) < 65504.f);
+          const float f = fast_exp2(m_ref[b] - mnew);
+#pragma unroll
+          for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) O[b][dt][r] *= f;
+          m_ref[b] = mnew;
+          set_mcol(b, mnew);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  constexpr std::false_type kNo{};
+  constexpr std::true_type kYes{};
+  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, kYes, kNo);
+  if (nfull == ntiles) tile(ntiles - 1, kNo, kNo);
+  else tile(ntiles - 1, kNo, kYes);
+
+  {
+    const bool any_bad = __any(bad || ovf);
+    if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
+  }
+  __syncthreads();
+  if (__builtin_expect(wg_flag != 0, 0)) {
+    // ---- exact recompute: bf16 Q and K as they are, S = Q K^T in f32, running max per
+    // 32-key sub-block with the defer-max rule (the sub-block's P V follows at once)
+    load_q(false);
+    float m_run[QB];
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      m_run[b] = -INFINITY;
+#pragma unroll
+      for (int dt = 0; dt < kNDT; ++dt) O[b][dt] = f32x16_t{};
+    }
+    for (int kt = 0; kt < ntiles; ++kt) {
+      stage_load(kt);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) stage_write(i, 0, false);
+      __syncthreads();
+      for (int sb = 0; sb < NSB; ++sb) {
+        short8_t kf[kNKT];
+        short8_t vf[2][kNDT];
+        read_k(Ks, sb, kf);
+        read_v(Vs, sb, vf);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) {
+          f32x16_t acc = f32x16_t{};
+#pragma unroll
+          for (int t = 0; t < kNKT; ++t) mma_bf16(acc, kf[t], qf[b][t]);
+          float sv[16];
+          float mx = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            sv[r] = (kt * BK + sb * 32 + acc_row(r, hh) < K) ? acc[r] * c : -INFINITY;
+            mx = fmaxf(mx, sv[r]);
+          }
+          mx = fmaxf(mx, other_half(mx));
+          if (!__all(mx <= m_run[b] + kThr)) {
+            const float mnew = fmaxf(m_run[b], mx);
+            const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m_run[b] - mnew);
+#pragma unroll
+            for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) O[b][dt][r] *= alpha;
+            m_run[b] = mnew;
+          }
+          short8_t pb[2];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pb[r >> 3][r & 7] = (short)f2bf(fast_exp2(sv[r] - m_run[b]));
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int dt = 0; dt < kNDT; ++dt) mma_bf16(O[b][dt], vf[s2][dt], pb[s2]);
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: O / l, rows 0-39 of O^T (q on the lane)
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const float l = __shfl(O[b][1][4], lane & 31);
+    const float inv = 1.f / l;
+    const int p = pw + 32 * b + qi;
+    if (p < a.P) {
+      uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * kD + (int64_t)p * a.ldo;
+#pragma unroll
+      for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = dt * 32 + 8 * g + 4 * hh;
+          if (dd < kD)
+            store4(op + dd, O[b][dt][4 * g] * inv, O[b][dt][4 * g + 1] * inv, O[b][dt][4 * g + 2] * inv,
+                   O[b][dt][4 * g + 3] * inv);
+        }
+    }
+  }
+}
+
+template <int WAVES, int QB, int BK, bool SCHED = true>
+hipError_t launch(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
+  hipLaunchKernelGGL((self40_kernel<WAVES, QB, BK, SCHED>), grid, block, 0, st, b);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool self40_eligible(const SelfArgs& a) { return a.P >= 2048 && a.K >= 256; }
+
+// variant: 0 = production shape; the experiments build also honours 62 (128-key tiles) and 64
+// (no scheduling directives)
+int run_self40(const SelfArgs& a, hipStream_t st) {
+#ifdef S40_ONLY
+  return (int)launch<S40_ONLY>(a, st);
+#else
+  switch (a.variant) {
+#ifdef P2P_EXPERIMENTS
+    case 62: return (int)launch<4, 2, 128>(a, st);
+    case 64: return (int)launch<4, 2, 256, false>(a, st);
+#endif
+    default: return (int)launch<4, 2, 256>(a, st);
+  }
+#endif
+}
+
+}  // namespace p2p

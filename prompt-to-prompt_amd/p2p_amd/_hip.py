@@ -12,8 +12,8 @@ from typing import Optional, Sequence
 import torch
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libp2p_hip.so")
-# A/B timing tools load the experiments build (make EXPERIMENTS=1 OUTDIR=../p2p_amd/exp) instead;
-# it is built from the same sources (check_source_hash holds for it too)
+# A/B timing tools load the experiments build (make EXPERIMENTS=1 -> p2p_amd/exp/) instead; it is
+# built from the same sources and stamped "<hash>-exp" (check_source_hash accepts it only here)
 if os.environ.get("P2P_EXPERIMENTS_LIB") == "1":
     _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "exp", "libp2p_hip.so")
 _lib = None
@@ -125,6 +125,8 @@ def check_source_hash() -> str:
     from . import _srchash
     built = lib().p2p_source_hash().decode()
     tree = _srchash.source_hash()
+    if os.environ.get("P2P_EXPERIMENTS_LIB") == "1":
+        tree += "-exp"   # the experiments build stamps its flavour (a production process refuses it)
     if built != tree:
         raise HipError(f"libp2p_hip.so was built from sources {built}, the tree has {tree}: rebuild "
                        f"(make -C prompt-to-prompt_amd/csrc)")

@@ -1,0 +1,61 @@
+#!/bin/bash
+# One GPU-box driver for every measurement this repo takes (run through gpurun from the repo
+# root).  Each step has its own time limit, steps are chained so the first failure, time-out or
+# fault ends the call, and everything lands under gpurun_out/<tag>/.
+#
+#   tools/gpu.sh <tag> <step> [<step> ...]
+#   steps:
+#     smoke                  __graft_entry__.smoke()
+#     tests[:<pytest -k>]    pytest -m gpu (optionally -k filtered)
+#     files:<f1,f2,..>       pytest -m gpu on the listed test files
+#     ab:<v1,v2,..>          G1 A/B (tools/g1_ab.py), one process per P2P_SELF_VARIANT (experiments lib)
+#     bench[:<args>]         python bench.py <args> (default: the driver's default run), JSON -> bench.json
+#     prof[:<args>]          rocprofv3 --kernel-trace --stats of bench.py <args>
+#     pmc:<name>:<counters>  one rocprofv3 --pmc pass over tools/g1_only.py (G1 launches only)
+#     cross                  tools/cross_bench.py (cross-attention launch shapes)
+#     py:<script>[:<args>]   python -u <script> <args>
+set -u
+export TMPDIR=/tmp
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+run() {  # run <seconds> <log> <cmd...>: time-limited, output to the log, tail on failure
+  local secs=$1 log=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1; local rc=$?
+  if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*"; tail -30 "$log"; exit $rc; fi
+}
+for step in "$@"; do
+  kind=${step%%:*}; arg=""; [ "$kind" != "$step" ] && arg=${step#*:}
+  echo "== $step"
+  case $kind in
+    smoke) run 300 "$out/smoke.log" python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$out/smoke.log" ;;
+    tests)
+      if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
+      run 1100 "$out/tests.log" python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests "${sel[@]}"
+      tail -1 "$out/tests.log" ;;
+    files)
+      run 1100 "$out/files.log" python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu ${arg//,/ }
+      tail -1 "$out/files.log" ;;
+    ab)
+      for v in ${arg//,/ }; do
+        run 150 "$out/ab_$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v python -u tools/g1_ab.py
+        tail -1 "$out/ab_$v.log" | tee -a "$out/ab.log"
+      done ;;
+    bench) run 900 "$out/bench.log" python -u bench.py $arg; grep '^{' "$out/bench.log" | tail -1 | tee "$out/bench.json" ;;
+    prof)
+      run 900 "$out/prof.log" rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 -u bench.py $arg
+      grep '^{' "$out/prof.log" | tail -1 | tee "$out/bench_under_rocprof.json"
+      find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \; ;;
+    pmc)
+      name=${arg%%:*}; counters=${arg#*:}
+      run 120 "$out/pmc_$name.log" timeout -s KILL 100 rocprofv3 --pmc ${counters//,/ } -d "$out/pmc_$name" -o run -- python3 -u tools/g1_only.py
+      find "$out/pmc_$name" -name "*counter_collection.csv" -exec cp {} "$out/pmc_$name.csv" \; ;;
+    cross) run 600 "$out/cross.log" python -u tools/cross_bench.py; tail -20 "$out/cross.log" ;;
+    py)
+      script=${arg%%:*}; sargs=""; [ "$script" != "$arg" ] && sargs=${arg#*:}
+      run 1100 "$out/py_$(basename "$script" .py).log" python -u "$script" $sargs
+      tail -15 "$out/py_$(basename "$script" .py).log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit 0
