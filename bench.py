@@ -207,8 +207,6 @@ def main():
     else:
         all_seeds = list(range(world * args.steps * G))
         warm_seeds = [10 ** 6 + rank * args.warmup * G + i for i in range(args.warmup * G)]
-    mine = sweep.partition(all_seeds, rank, world)
-    timed = [mine[i:i + G] for i in range(0, len(mine), G)]
     for i in range(args.warmup):
         batch(warm_seeds[i * G:(i + 1) * G])
     if world > 1:
@@ -216,15 +214,15 @@ def main():
     torch.cuda.synchronize(dev)
     timer.enabled = True
     t0 = time.perf_counter()
-    outs = []
-    for i, b in enumerate(timed):
-        outs.append(batch(b))
-        if len(timed) > 4:   # long sweeps: a progress line per batch (stderr; host-side only)
-            print(f"[bench rank {rank}] batch {i + 1}/{len(timed)}", file=sys.stderr, flush=True)
-    lats = torch.cat([o[0] for o in outs]).float() if outs else torch.zeros(0, B, 4, 64, 64, device=dev)
-    maps = torch.cat([o[1] for o in outs]).float() if outs else torch.zeros(0, B, 16, 16, 77, device=dev)
-    # ONE RCCL all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
-    lat_all, maps_all = sweep.gather_results([lats, maps], len(all_seeds), world)
+
+    def progress(i, n):   # long sweeps: a progress line per batch (stderr; host-side only)
+        if n > 4:
+            print(f"[bench rank {rank}] batch {i + 1}/{n}", file=sys.stderr, flush=True)
+
+    # the sweep tests/test_distributed.py runs over gloo: this rank's batches, then ONE RCCL
+    # all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
+    lat_all, maps_all = sweep.run_batched_sweep(all_seeds, batch, [(B, 4, 64, 64), (B, 16, 16, 77)], rank, world, G,
+                                                device=dev, on_batch=progress)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -255,7 +253,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.ddim_steps)
-        n_steps = max(1, (len(sweep.partition(all_seeds, 0, world)) + G - 1) // G)
+        n_steps = max(1, len(sweep.batches(all_seeds, 0, world, G)))
         workload = ("configs[3]: seed sweep of " + str(n_total) + " edit groups, " if args.seeds > 0 else
                     "configs[1]: ")
         line = {

@@ -10,7 +10,7 @@ all-gather (RCCL over xGMI on GPUs, gloo on CPU).
 """
 from __future__ import annotations
 
-from typing import Callable, List, Sequence, Tuple, Union
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
@@ -59,22 +59,46 @@ def gather_results(local: Sequence[torch.Tensor], n_total: int, world: int) -> L
     return outs
 
 
-def run_sweep(seeds: Sequence[int], run_group: Callable[[int], Result], rank: int = 0,
-              world: int = 1) -> Result:
-    """Run this rank's share of the groups; every rank returns every group's results in seed
-    order.  run_group(seed) returns one tensor (the final latents) or a tuple of tensors
-    (latents, reduced maps, ...); the return value has the same structure, stacked over seeds."""
+def batches(seeds: Sequence[int], rank: int, world: int, groups_per_call: int) -> List[List[int]]:
+    """This rank's seeds (round-robin shard) cut into batches of at most groups_per_call groups,
+    each batch one U-Net call per denoising step (controllers.GroupBatch)."""
     mine = partition(seeds, rank, world)
-    outs = [run_group(s) for s in mine]
-    if not outs:
-        outs_probe = run_group(seeds[0])
-        single = isinstance(outs_probe, torch.Tensor)
-        probe = (outs_probe,) if single else tuple(outs_probe)
-        local = [p.new_zeros((0,) + tuple(p.shape)) for p in probe]
+    return [mine[i:i + groups_per_call] for i in range(0, len(mine), groups_per_call)]
+
+
+def run_batched_sweep(seeds: Sequence[int], run_batch: Callable[[List[int]], Sequence[torch.Tensor]],
+                      out_shapes: Sequence[Tuple[int, ...]], rank: int = 0, world: int = 1,
+                      groups_per_call: int = 1, device=None,
+                      on_batch: Optional[Callable[[int, int], None]] = None) -> Tuple[torch.Tensor, ...]:
+    """The sweep bench.py times (configs[3]) and tests/test_distributed.py runs over gloo: this
+    rank's share of the groups in batches of groups_per_call, then ONE all-gather of every
+    result.  run_batch(seeds) returns one tensor per result, each [len(seeds), *out_shapes[i]]
+    (e.g. final latents and reduced maps).  Every rank returns every group's results in seed
+    order, as f32 [len(seeds), *out_shapes[i]].  A rank with no seeds contributes empty stacks
+    of the given shapes (nothing is run to learn them)."""
+    todo = batches(seeds, rank, world, groups_per_call)
+    outs = []
+    for i, b in enumerate(todo):
+        res = tuple(run_batch(b))
+        if len(res) != len(out_shapes) or any(tuple(r.shape) != (len(b),) + tuple(sh)
+                                               for r, sh in zip(res, out_shapes)):
+            raise ValueError(f"run_batch returned {[tuple(r.shape) for r in res]}, expected "
+                             f"{[(len(b),) + tuple(sh) for sh in out_shapes]}")
+        outs.append(res)
+        if on_batch is not None:
+            on_batch(i, len(todo))
+    if outs:
+        local = [torch.cat([o[j].float() for o in outs]) for j in range(len(out_shapes))]
     else:
-        single = isinstance(outs[0], torch.Tensor)
-        cols = [(o,) if single else tuple(o) for o in outs]
-        local = [torch.stack([c[i] for c in cols]) for i in range(len(cols[0]))]
-    if single:
-        return gather_latents(local[0], len(seeds), world)
+        local = [torch.zeros((0,) + tuple(sh), device=device) for sh in out_shapes]
     return tuple(gather_results(local, len(seeds), world))
+
+
+def run_sweep(seeds: Sequence[int], run_group: Callable[[int], Result], out_shapes: Sequence[Tuple[int, ...]],
+              rank: int = 0, world: int = 1, device=None) -> Tuple[torch.Tensor, ...]:
+    """One group per call: run_group(seed) returns a tensor or a tuple of tensors of out_shapes."""
+    def run_batch(b):
+        r = run_group(b[0])
+        r = (r,) if isinstance(r, torch.Tensor) else tuple(r)
+        return tuple(t[None] for t in r)
+    return run_batched_sweep(seeds, run_batch, out_shapes, rank, world, 1, device)

@@ -58,14 +58,24 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, seeds, out_path):
+OUT_SHAPES = [(4, 4, 32, 32), (4, 16, 16, 77)]
+
+
+def run_batch(model, seeds):
+    """A batch of groups, as bench.py's batch(): results stacked [len(seeds), ...]."""
+    res = [real_group(model, s) for s in seeds]
+    return torch.stack([r[0] for r in res]), torch.stack([r[1] for r in res])
+
+
+def _worker(rank, world, port, seeds, gpc, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         model = tiny_model()
-        lat, maps = sweep.run_sweep(seeds, lambda s: real_group(model, s), rank, world)
+        # the function bench.py times: shard, batches of gpc groups, ONE all-gather
+        lat, maps = sweep.run_batched_sweep(seeds, lambda b: run_batch(model, b), OUT_SHAPES, rank, world, gpc)
         if rank == 0:
             torch.save({"lat": lat, "maps": maps}, out_path)
     finally:
@@ -85,17 +95,32 @@ def test_gather_results_single_process_is_identity():
     assert torch.equal(x, a) and torch.equal(y, b)
 
 
-@pytest.mark.parametrize("world,n", [(2, 3), (3, 4)])
-def test_gloo_sweep_real_groups_matches_single_process(tmp_path, world, n):
+def test_batches_cover_every_seed_once():
+    seeds = list(range(11))
+    got = [sweep.batches(seeds, r, 3, 2) for r in range(3)]
+    assert got[0] == [[0, 3], [6, 9]] and got[2] == [[2, 5], [8]]
+    assert sorted(s for r in got for b in r for s in b) == seeds
+
+
+def test_rank_without_seeds_runs_nothing():
+    """A rank whose shard is empty contributes empty stacks of the declared shapes; no group
+    is run to learn them (the gloo cases below cover such a rank inside a real gather)."""
+    calls = []
+    out = sweep.run_batched_sweep([], lambda b: calls.append(b), OUT_SHAPES)
+    assert calls == [] and [tuple(t.shape) for t in out] == [(0,) + s for s in OUT_SHAPES]
+
+
+@pytest.mark.parametrize("world,n,gpc", [(2, 3, 1), (3, 4, 1), (2, 5, 2), (3, 2, 1)])   # (3, 2): rank 2 empty
+def test_gloo_sweep_real_groups_matches_single_process(tmp_path, world, n, gpc):
     seeds = [11 * i + 3 for i in range(n)]
     out = str(tmp_path / "res.pt")
-    mp.spawn(_worker, args=(world, _free_port(), seeds, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), seeds, gpc, out), nprocs=world, join=True)
     got = torch.load(out, weights_only=True)
     threads = torch.get_num_threads()
     torch.set_num_threads(2)        # the workers' thread count: same CPU reduction order, same bits
     try:
         model = tiny_model()
-        want_lat, want_maps = sweep.run_sweep(seeds, lambda s: real_group(model, s))
+        want_lat, want_maps = sweep.run_sweep(seeds, lambda s: real_group(model, s), OUT_SHAPES)
     finally:
         torch.set_num_threads(threads)
     assert got["lat"].shape == (n, 4, 4, 32, 32)
