@@ -18,8 +18,9 @@
 // the same bf16 p that P V uses.  The reference point m of a query row is the maximum over the
 // first 32 keys (no per-tile maximum); a tile whose row sum passes 2^64 moves m up by 64 and
 // rescales O by the exact factor.  Anything outside the fast form's range -- |c q| or |k| past
-// the f16 range, |m| >= 65504, a non-finite row sum -- flags the workgroup, which recomputes
-// everything on the exact bf16 path (unscaled bf16 Q and K, running max per sub-block).
+// the f16 range, |m| >= 65504, a non-finite row sum or O element -- flags the workgroup, which
+// recomputes everything on the exact bf16 path (unscaled bf16 Q and K, running max per
+// sub-block).
 #include <type_traits>
 #include <utility>
 
@@ -59,9 +60,16 @@ __device__ __forceinline__ void mma_bf16(f32x16_t& acc, const short8_t& a, const
                                                 0, 0, 0);
 }
 
+#ifdef P2P_EXPERIMENTS
+// Diagnostic build (FORM bit 16, experiments library only): per-wave shader-clock stamps of the
+// first 256 workgroups, read back by p2p_diag_self40_stamps (tools/s40_stamps.py).
+constexpr int kStampSlots = 40;
+__device__ unsigned long long g_s40_stamps[256 * 8 * kStampSlots];
+#endif
+
 // One workgroup = WAVES waves x QB query blocks of 32 rows = 32*QB*WAVES queries of one (entry,
 // head); BK-key tiles, double-buffered in LDS.
-template <int WAVES, int QB, int BK, bool SCHED>
+template <int WAVES, int QB, int BK, bool SCHED, int FORM>
 __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(SelfArgs a) {
   constexpr int NSB = BK / 32;
   constexpr int NT = 64 * WAVES;
@@ -70,9 +78,19 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   constexpr int VBUF = BK * kVS;
   constexpr int X = NSB * QB;   // pipeline steps (32x32 blocks) per tile
   constexpr float kThr = 8.0f;  // exact path: defer-max threshold (log2 units)
-  constexpr int kHalf = X / 2;  // staging writes start here, one chunk every kSpread steps
-  constexpr int kSpread = (X - kHalf) / NCH > 0 ? (X - kHalf) / NCH : 1;
-  static_assert(kHalf + (NCH - 1) * kSpread < X, "every staged chunk is written inside the tile");
+  // FORM bit 128 (split staging): waves 0..WAVES/2-1 stage K (the f16 conversion), the younger
+  // half -- the VALU-arbitration loser -- stages V (copy only); else every wave stages both
+  constexpr bool kSplit = (FORM & 128) != 0;
+  constexpr int SCH = (BK * kCPR + NT / 2 - 1) / (NT / 2);   // chunks per thread, split staging
+  constexpr int CMAX = kSplit ? SCH : NCH;
+  constexpr int kHalf = X / 2;  // staging writes start here, one chunk every spread(role) steps
+  auto nchunks = [](auto role) { return decltype(role)::value == 0 ? NCH : SCH; };
+  auto spread = [](auto role) {
+    constexpr int n = decltype(role)::value == 0 ? NCH : SCH;
+    return (X - kHalf) / n > 0 ? (X - kHalf) / n : 1;
+  };
+  static_assert(kHalf + (NCH - 1) * ((X - kHalf) / NCH > 0 ? (X - kHalf) / NCH : 1) < X, "chunks fit the tile");
+  static_assert(!kSplit || kHalf + (SCH - 1) * ((X - kHalf) / SCH > 0 ? (X - kHalf) / SCH : 1) < X, "chunks fit");
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2 * KBUF];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[2 * VBUF];
   __shared__ int wg_flag;
@@ -84,6 +102,14 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   const int qi = lane & 31;
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  auto stamp = [&](int idx) __attribute__((always_inline)) {
+#ifdef P2P_EXPERIMENTS
+    if constexpr ((FORM & 16) != 0)
+      if (logical < 256 && lane == 0 && idx < kStampSlots)
+        g_s40_stamps[(logical * WAVES + wave) * kStampSlots + idx] = __builtin_amdgcn_s_memtime();
+#endif
+  };
+  stamp(0);
   const int qt = logical % a.n_qtiles;
   const int nh = logical / a.n_qtiles;
   const int h = nh % a.H;
@@ -139,41 +165,54 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     if (hh == 1) qf[b][2][0] = (short)__builtin_bit_cast(uint16_t, (_Float16)(-m));
   };
 
-  // ---- K/V staging: chunk i of this thread = row cidx / 5, 16-byte chunk cidx % 5
-  short8_t kreg[NCH], vreg[NCH];
-  uint32_t koff[NCH], voff[NCH];
-  int lrow[NCH], lch[NCH];
+  // ---- K/V staging: chunk i of this thread = row cidx / 5, 16-byte chunk cidx % 5 (role 0: both
+  // K and V of the chunk; split staging: role 1 = K chunks of threads 0..NT/2-1, role 2 = V
+  // chunks of the others, each thread holding SCH of them in kreg)
+  const bool young = __builtin_amdgcn_readfirstlane(wave) >= WAVES / 2;
+  const int stid = kSplit ? tid - (young ? NT / 2 : 0) : tid;
+  const int sstride = kSplit ? NT / 2 : NT;
+  short8_t kreg[CMAX], vreg[NCH];
+  uint32_t koff[CMAX], voff[NCH];
+  int lrow[CMAX], lch[CMAX];
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int cidx = tid + i * NT;
+  for (int i = 0; i < CMAX; ++i) {
+    const int cidx = stid + i * sstride;
     const int row = min(cidx / kCPR, BK - 1);
     const int ch = cidx - (cidx / kCPR) * kCPR;
     lrow[i] = row;
     lch[i] = ch;
-    koff[i] = (uint32_t)((row * (int)a.ldk + ch * 8) * 2);
-    voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
+    koff[i] = (uint32_t)((row * (int)(kSplit && young ? a.ldv : a.ldk) + ch * 8) * 2);
+    if (i < NCH) voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
   }
   const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + kD) * 2;
   const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + kD) * 2;
   const int64_t kstep = (int64_t)BK * a.ldk * 2;
   const int64_t vstep = (int64_t)BK * a.ldv * 2;
-  auto chunk_live = [&](int i) __attribute__((always_inline)) {
-    return (BK * kCPR) % NT == 0 || tid + i * NT < BK * kCPR;
+  auto chunk_live = [&](int i, auto role) __attribute__((always_inline)) {
+    constexpr int sn = decltype(role)::value == 0 ? NT : NT / 2;
+    return (BK * kCPR) % sn == 0 || stid + i * sn < BK * kCPR;
   };
-  auto stage_load = [&](int kt) __attribute__((always_inline)) {
+  auto stage_load = [&](int kt, auto role) __attribute__((always_inline)) {
+    constexpr int kRole = decltype(role)::value;
     const __amdgpu_buffer_rsrc_t rk = make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
     const __amdgpu_buffer_rsrc_t rv = make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      if (chunk_live(i)) {
-        kreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)koff[i], 0, 0));
-        vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)voff[i], 0, 0));
+    for (int i = 0; i < nchunks(role); ++i)
+      if (chunk_live(i, role)) {
+        kreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(kRole == 2 ? rv : rk, (int)koff[i], 0, 0));
+        if constexpr (kRole == 0)
+          vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)voff[i], 0, 0));
       }
   };
   // chunk i into LDS buffer buf: K as f16 (fast form; exact inside the f16 range, RTZ packing
   // would clamp past 65504 silently, so the range is checked) or raw bf16 (exact path)
-  auto stage_write = [&](int i, int buf, bool as_f16) __attribute__((always_inline)) {
-    if (!chunk_live(i)) return;
+  auto stage_write = [&](int i, int buf, bool as_f16, auto role) __attribute__((always_inline)) {
+    constexpr int kRole = decltype(role)::value;
+    if (!chunk_live(i, role)) return;
+    if constexpr (kRole == 2) {
+      *reinterpret_cast<short8_t*>(Vs + buf * VBUF + lrow[i] * kVS + lch[i] * 8) = kreg[i];
+      return;
+    }
     uint16_t* const kd = Ks + buf * KBUF + lrow[i] * kKS + lch[i] * 8;
     if (as_f16) {
       short8_t hv;
@@ -191,7 +230,18 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     } else {
       *reinterpret_cast<short8_t*>(kd) = kreg[i];
     }
-    *reinterpret_cast<short8_t*>(Vs + buf * VBUF + lrow[i] * kVS + lch[i] * 8) = vreg[i];
+    if constexpr (kRole == 0) *reinterpret_cast<short8_t*>(Vs + buf * VBUF + lrow[i] * kVS + lch[i] * 8) = vreg[i];
+  };
+  // a whole tile into buf, for the role(s) of this wave (prologue and exact recompute)
+  auto stage_all = [&](int kt, int buf, bool as_f16) __attribute__((always_inline)) {
+    auto go = [&](auto role) __attribute__((always_inline)) {
+      stage_load(kt, role);
+#pragma unroll
+      for (int i = 0; i < nchunks(role); ++i) stage_write(i, buf, as_f16, role);
+    };
+    if constexpr (!kSplit) go(std::integral_constant<int, 0>{});
+    else if (young) go(std::integral_constant<int, 2>{});
+    else go(std::integral_constant<int, 1>{});
   };
 
   const int ntiles = (K + BK - 1) / BK;
@@ -215,9 +265,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       for (int dt = 0; dt < kNDT; ++dt) vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
   };
 
-  stage_load(0);
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) stage_write(i, 0, true);
+  stage_all(0, 0, true);
   __syncthreads();
 
   // ---- reference point: the row maximum of c s over the first 32 keys (Q column 40 is still 0)
@@ -240,35 +288,54 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     }
   }
 
+  stamp(1);
+  // static priority for the second-dispatched half of the waves (FORM bit 8; the condition must
+  // be provably wave-uniform, or every wave gets priority 1)
+  if constexpr ((FORM & 8) != 0)
+    if (__builtin_amdgcn_readfirstlane(wave) >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+  // FORM bits 32/64: the waves sharing a SIMD (w, w + WAVES/2) run the same program; the older
+  // one wins VALU arbitration and reaches the tile barrier first.  The younger half takes
+  // priority 1 for the first kFlip steps of every tile, so both arrive together
+  constexpr int kFlipSel = (FORM >> 5) & 3;
+  constexpr int kFlip = kFlipSel == 1 ? X / 2 : kFlipSel == 2 ? X / 4 : kFlipSel == 3 ? (3 * X) / 4 : 0;
   bool bad = false;
   // ---- one tile of the fast form, software-pipelined over its X blocks.  more: the next tile
   // is staged during this one (compile-time, so the tile body is one basic block); masked: keys
   // past K in this tile
-  auto tile = [&](int kt, auto more, auto masked) __attribute__((always_inline)) {
+  auto tile = [&](int kt, auto more, auto masked, auto role) __attribute__((always_inline)) {
     constexpr bool kMore = decltype(more)::value;
     constexpr bool kMasked = decltype(masked)::value;
+    constexpr int kSpread = spread(role);
+    constexpr int kNcw = nchunks(role);
     const int buf = kt & 1;
-    if constexpr (kMore) stage_load(kt + 1);
+    if constexpr (kMore) stage_load(kt + 1, role);
     const uint16_t* const Kb = Ks + buf * KBUF;
     const uint16_t* const Vb = Vs + buf * VBUF;
+    // LEAN: one K and one V fragment set, each re-read right after its last reader (K of
+    // sub-block sb+1 after the last Q K^T on sb, V of sb after the last P V on sb-1)
+    constexpr bool kLean = (FORM & 1) != 0;
+    constexpr bool kLeanK = kLean && (FORM & 4) == 0;   // FORM bit 4: LEAN V, double-buffered K
+    constexpr bool kValuFirst = (FORM & 2) != 0;
     short8_t kf[2][kNKT];
     short8_t vf[2][2][kNDT];
     f32x16_t S[2];
     short8_t pf[2][2];
     read_k(Kb, 0, kf[0]);
     read_v(Vb, 0, vf[0]);
+    auto kslot = [](int sb) { return kLeanK ? 0 : (sb & 1); };
+    auto vslot = [](int sb) { return kLean ? 0 : (sb & 1); };
     auto qk = [&](int x) __attribute__((always_inline)) {
       const int sb = x / QB, b = x % QB;
       S[x & 1] = f32x16_t{};
 #pragma unroll
-      for (int t = 0; t < kNKT; ++t) mma_f16(S[x & 1], kf[sb & 1][t], qf[b][t]);
+      for (int t = 0; t < kNKT; ++t) mma_f16(S[x & 1], kf[kslot(sb)][t], qf[b][t]);
     };
     auto pv = [&](int x) __attribute__((always_inline)) {
       const int sb = x / QB, b = x % QB;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int dt = 0; dt < kNDT; ++dt) mma_bf16(O[b][dt], vf[sb & 1][s2][dt], pf[x & 1][s2]);
+        for (int dt = 0; dt < kNDT; ++dt) mma_bf16(O[b][dt], vf[vslot(sb)][s2][dt], pf[x & 1][s2]);
     };
     auto ex = [&](int x) __attribute__((always_inline)) {
       const int sb = x / QB;
@@ -285,42 +352,71 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) pf[x & 1][s2][j] = (short)f2bf(e[8 * s2 + j]);
     };
+    if constexpr (kFlip > 0)
+      if (young) __builtin_amdgcn_s_setprio(1);
     qk(0);
     if constexpr (SCHED) __builtin_amdgcn_sched_barrier(0);
     static_for<X>([&](auto xc) __attribute__((always_inline)) {
       constexpr int x = decltype(xc)::value;
+      if constexpr (kFlip > 0 && x == kFlip)
+        if (young) __builtin_amdgcn_s_setprio(0);
+      // FORM bit 256: the younger half holds priority 1 for the first half of every kAlt steps
+      // (bit 512: kAlt = 4, else 2), so the two waves of a SIMD share the VALU evenly
+      if constexpr ((FORM & 256) != 0) {
+        constexpr int kAlt = (FORM & 512) ? 4 : 2;
+        if constexpr (x % kAlt == 0) { if (young) __builtin_amdgcn_s_setprio(1); }
+        if constexpr (x % kAlt == kAlt / 2) { if (young) __builtin_amdgcn_s_setprio(0); }
+      }
       constexpr int sb = x / QB, b = x % QB;
-      constexpr bool kRdK = b == 0 && sb + 1 < NSB;
-      constexpr bool kRdV = b == (QB > 1 ? 1 : 0) && sb + 1 < NSB;
+      // K of sub-block sb+1: LEAN after this step's Q K^T when it was the last one on sb
+      // (b == QB-2: Q K^T of block x+1 = (sb, QB-1)), else early into the other slot
+      constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSB;
+      // V: LEAN reads V(sb) after this step's P V on block x-1 = (sb-1, QB-1); else V(sb+1) early
+      constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSB);
       // the next tile's chunks go to the other buffer over the second half of the tile (every
       // wave has passed the barrier that ended the tile which last read that buffer)
-      constexpr bool kStw = kMore && x >= kHalf && (x - kHalf) % kSpread == 0 && (x - kHalf) / kSpread < NCH;
-      if constexpr (kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
-      if constexpr (kRdV) read_v(Vb, sb + 1, vf[(sb + 1) & 1]);
+      constexpr bool kStw = kMore && x >= kHalf && (x - kHalf) % kSpread == 0 && (x - kHalf) / kSpread < kNcw;
+      constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
+      if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
+      if constexpr (!kLean && kRdV) read_v(Vb, sb + 1, vf[(sb + 1) & 1]);
       if constexpr (x + 1 < X) qk(x + 1);
       ex(x);
+      if constexpr (kLeanK && kRdK) read_k(Kb, sb + 1, kf[0]);
       if constexpr (x >= 1) pv(x - 1);
-      if constexpr (kStw) stage_write((x - kHalf) / kSpread, buf ^ 1, true);
+      if constexpr (kLean && kRdV) read_v(Vb, sb, vf[0]);
+      if constexpr (kStw) stage_write((x - kHalf) / kSpread, buf ^ 1, true, role);
       if constexpr (SCHED) {
-        // one MFMA per slot, the step's VALU spread evenly over the slots, LDS reads early
+        // one MFMA per slot (this step's Q K^T first, then P V), the step's exponentials and
+        // VALU spread evenly over the slots; LDS reads early, or (LEAN) after their last reader
         // (masks: MFMA 0x8, VALU 0x2 -- which excludes the transcendental v_exp --, TRANS
         // 0x400, DS_READ 0x100, DS_WRITE 0x200)
-        constexpr int nm = (x + 1 < X ? kNKT : 0) + (x >= 1 ? 2 * kNDT : 0);
+        constexpr int nq = x + 1 < X ? kNKT : 0;
+        constexpr int nm = nq + (x >= 1 ? 2 * kNDT : 0);
         constexpr int ne = 16;
-        constexpr int nv = 8 + (kStw ? 24 : 0) + (kMasked ? 32 : 0);
-        constexpr int nr = (kRdK ? kNKT : 0) + (kRdV ? 8 : 0);
+        constexpr int nv = 8 + (kStwK ? 24 : 0) + (kMasked ? 32 : 0);
+        constexpr int nr = (!kLeanK && kRdK ? kNKT : 0) + (!kLean && kRdV ? 8 : 0);
         static_for<nm>([&](auto ic) __attribute__((always_inline)) {
           constexpr int i = decltype(ic)::value;
+          constexpr int te = (ne * (i + 1)) / nm - (ne * i) / nm;
+          constexpr int tv = (nv * (i + 1)) / nm - (nv * i) / nm;
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x400, (ne * (i + 1)) / nm - (ne * i) / nm, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, (nv * (i + 1)) / nm - (nv * i) / nm, 0);
+          if constexpr (kValuFirst) {
+            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
+            __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
+          } else {
+            __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
+          }
           if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, (nr * (i + 1)) / nm - (nr * i) / nm, 0);
+          if constexpr (kLeanK && kRdK && i >= nq && i < nq + kNKT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           if constexpr (kStw && i < 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         });
+        if constexpr (kLean && kRdV) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     });
     pv(X - 1);
+    stamp(2 + 2 * kt);
     // row sums (O^T row 40 = d tile 1, register 4 of the low lane half): a sum past 2^64 moves
     // the reference point up by 64 (rounded to f16) and rescales O by the exact factor
 #pragma unroll
@@ -343,14 +439,30 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       }
     }
     __syncthreads();
+    stamp(3 + 2 * kt);
   };
   constexpr std::false_type kNo{};
   constexpr std::true_type kYes{};
-  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, kYes, kNo);
-  if (nfull == ntiles) tile(ntiles - 1, kNo, kNo);
-  else tile(ntiles - 1, kNo, kYes);
+  auto run_tiles = [&](auto role) __attribute__((always_inline)) {
+    for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, kYes, kNo, role);
+    if (nfull == ntiles) tile(ntiles - 1, kNo, kNo, role);
+    else tile(ntiles - 1, kNo, kYes, role);
+  };
+  if constexpr (!kSplit) run_tiles(std::integral_constant<int, 0>{});
+  else if (young) run_tiles(std::integral_constant<int, 2>{});
+  else run_tiles(std::integral_constant<int, 1>{});
 
   {
+    // a row sum can stay finite while an O element overflowed (p near 2^128 times a large |v|):
+    // any non-finite accumulator also sends the workgroup to the exact recompute
+    float nf = 0.f;
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nf = __builtin_fmaf(O[b][dt][r], 0.f, nf);   // NaN iff some O is inf/NaN
+    bad |= !(nf == 0.f);
     const bool any_bad = __any(bad || ovf);
     if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
   }
@@ -367,9 +479,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       for (int dt = 0; dt < kNDT; ++dt) O[b][dt] = f32x16_t{};
     }
     for (int kt = 0; kt < ntiles; ++kt) {
-      stage_load(kt);
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) stage_write(i, 0, false);
+      stage_all(kt, 0, false);
       __syncthreads();
       for (int sb = 0; sb < NSB; ++sb) {
         short8_t kf[kNKT];
@@ -411,6 +521,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     }
   }
 
+  stamp(36);
   // ---- epilogue: O / l, rows 0-39 of O^T (q on the lane)
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
@@ -430,14 +541,15 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
         }
     }
   }
+  stamp(37);
 }
 
-template <int WAVES, int QB, int BK, bool SCHED = true>
+template <int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
 hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
-  hipLaunchKernelGGL((self40_kernel<WAVES, QB, BK, SCHED>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self40_kernel<WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -455,10 +567,35 @@ int run_self40(const SelfArgs& a, hipStream_t st) {
 #ifdef P2P_EXPERIMENTS
     case 62: return (int)launch<4, 2, 128>(a, st);
     case 64: return (int)launch<4, 2, 256, false>(a, st);
+    case 61: return (int)launch<4, 2, 256>(a, st);
+    case 67: return (int)launch<8, 2, 256, true, 3>(a, st);
+    case 68: return (int)launch<4, 2, 256, true, 2>(a, st);
+    case 69: return (int)launch<4, 2, 256, true, 1>(a, st);
+    case 70: return (int)launch<8, 2, 128, true, 1>(a, st);
+    case 71: return (int)launch<8, 2, 256, true, 1 | 16>(a, st);   // the default shape with clock stamps
+    case 72: return (int)launch<8, 2, 256, true, 1 | 8>(a, st);
+    case 73: return (int)launch<8, 2, 256, true, 1 | 4>(a, st);
+    case 74: return (int)launch<8, 2, 256, true, 1 | 32>(a, st);        // priority flip at X/2
+    case 75: return (int)launch<8, 2, 256, true, 1 | 64>(a, st);        // at X/4
+    case 76: return (int)launch<8, 2, 256, true, 1 | 96>(a, st);        // at 3X/4
+    case 77: return (int)launch<8, 2, 256, true, 1 | 32 | 16>(a, st);   // 74 with clock stamps
+    case 78: return (int)launch<8, 2, 256, true, 1 | 128>(a, st);       // split staging
+    case 79: return (int)launch<8, 2, 256, true, 1 | 128 | 32>(a, st);  // split staging + flip at X/2
+    case 80: return (int)launch<8, 2, 256, true, 1 | 128 | 16>(a, st);  // 78 with clock stamps
+    case 81: return (int)launch<8, 2, 256, true, 1 | 128 | 256>(a, st);        // split + alternate every 2 steps
+    case 82: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // split + alternate every 4 steps
+    case 83: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // 81 with clock stamps
 #endif
-    default: return (int)launch<4, 2, 256>(a, st);
+    default: return (int)launch<8, 2, 256, true, 1>(a, st);
   }
 #endif
 }
 
 }  // namespace p2p
+
+#ifdef P2P_EXPERIMENTS
+extern "C" int p2p_diag_self40_stamps(void* dst, int64_t bytes) {
+  const int64_t n = (int64_t)sizeof(p2p::g_s40_stamps);
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(p2p::g_s40_stamps), bytes < n ? bytes : n, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -11,7 +11,8 @@
 #     ab:<v1,v2,..>          G1 A/B (tools/g1_ab.py), one process per P2P_SELF_VARIANT (experiments lib)
 #     bench[:<args>]         python bench.py <args> (default: the driver's default run), JSON -> bench.json
 #     prof[:<args>]          rocprofv3 --kernel-trace --stats of bench.py <args>
-#     pmc:<name>:<counters>  one rocprofv3 --pmc pass over tools/g1_only.py (G1 launches only)
+#     pmc:<name>:<counters>  one rocprofv3 --pmc pass (comma-separated counters) over tools/g1_only.py
+#                            (G1 launches only; P2P_SELF_VARIANT / P2P_EXPERIMENTS_LIB from the env)
 #     cross                  tools/cross_bench.py (cross-attention launch shapes)
 #     py:<script>[:<args>]   python -u <script> <args>
 set -u
@@ -48,8 +49,9 @@ for step in "$@"; do
       find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \; ;;
     pmc)
       name=${arg%%:*}; counters=${arg#*:}
-      run 120 "$out/pmc_$name.log" timeout -s KILL 100 rocprofv3 --pmc ${counters//,/ } -d "$out/pmc_$name" -o run -- python3 -u tools/g1_only.py
-      find "$out/pmc_$name" -name "*counter_collection.csv" -exec cp {} "$out/pmc_$name.csv" \; ;;
+      run 120 "$out/pmc_$name.log" timeout -s KILL 100 rocprofv3 --pmc ${counters//,/ } --output-format csv -d "$out/pmc_$name" -o run -- python3 -u tools/g1_only.py
+      f=$(find "$out/pmc_$name" -name "*counter_collection.csv" | head -1)
+      [ -n "$f" ] && python3 tools/pmc_summary.py "$f" | tee -a "$out/pmc_summary.txt" ;;
     cross) run 600 "$out/cross.log" python -u tools/cross_bench.py; tail -20 "$out/cross.log" ;;
     py)
       script=${arg%%:*}; sargs=""; [ "$script" != "$arg" ] && sargs=${arg#*:}

@@ -11,7 +11,7 @@ def main(path):
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "?")
-            short = name.split("(")[0][-90:]
+            short = name.replace("(anonymous namespace)::", "").split("(")[0][-90:]
             disp = int(row.get("Dispatch_Id", 0))
             vals[short][row["Counter_Name"]][disp] = float(row["Counter_Value"])
     for kern, counters in vals.items():

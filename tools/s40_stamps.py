@@ -1,0 +1,68 @@
+"""Where a wave of the d = 40 self-attention kernel spends its cycles (experiments build, variant
+71 = the production shape with s_memtime stamps): prologue, per-tile compute, barrier wait per
+tile, recompute check + epilogue.  Stamps come from the first 256 workgroups of a config-2 G1
+launch (N = 8, H = 8, P = K = 4096, d = 40).
+Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=71 python tools/s40_stamps.py"""
+import ctypes
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "prompt-to-prompt_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from p2p_amd import _hip  # noqa: E402
+
+SLOTS, WAVES, NWG, NTILES = 40, 8, 256, 16
+
+
+def main():
+    N, H, P, d = 8, 8, 4096, 40
+    C = H * d
+    q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    k = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    v = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    o = torch.empty_like(q)
+    for _ in range(20):
+        _hip.self_attn(q, k, v, o, H, d ** -0.5)
+    torch.cuda.synchronize()
+    buf = np.zeros(NWG * WAVES * SLOTS, dtype=np.uint64)
+    fn = _hip.lib().p2p_diag_self40_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    rc = fn(buf.ctypes.data, buf.nbytes)
+    assert rc == 0, rc
+    st = buf.reshape(NWG, WAVES, SLOTS).astype(np.int64)
+    t0 = st[:, :, 0]
+    pro = st[:, :, 1] - t0
+    comp, bar = [], []
+    prev = st[:, :, 1]
+    for kt in range(NTILES):
+        e, b = st[:, :, 2 + 2 * kt], st[:, :, 3 + 2 * kt]
+        comp.append(e - prev)
+        bar.append(b - e)
+        prev = b
+    comp, bar = np.stack(comp, -1), np.stack(bar, -1)
+    chk = st[:, :, 36] - prev
+    epi = st[:, :, 37] - st[:, :, 36]
+    tot = st[:, :, 37] - t0
+    med = lambda a: float(np.median(a))  # noqa: E731
+    print(f"cycles per wave (median over {NWG} workgroups x {WAVES} waves):")
+    print(f"  total {med(tot):.0f}  prologue {med(pro):.0f}  compute/tile {med(comp):.0f} (x{NTILES} = {med(comp.sum(-1)):.0f})"
+          f"  barrier/tile {med(bar):.0f} (x{NTILES} = {med(bar.sum(-1)):.0f})  check {med(chk):.0f}  epilogue {med(epi):.0f}")
+    print(f"  compute per 32x32 block: {med(comp) / 16:.0f} cycles per wave (2 waves per SIMD)")
+    print(f"  tile 0 compute {med(comp[..., 0]):.0f}, tiles 1-{NTILES - 1} {med(comp[..., 1:]):.0f}")
+    # younger half vs older half
+    print(f"  waves 0-3 compute/tile {med(comp[:, :4]):.0f} barrier/tile {med(bar[:, :4]):.0f};"
+          f" waves 4-7 compute/tile {med(comp[:, 4:]):.0f} barrier/tile {med(bar[:, 4:]):.0f}")
+    # skew of barrier arrival within a workgroup
+    arr = st[:, :, 2:2 + 2 * NTILES:2]
+    skew = arr.max(1) - arr.min(1)
+    print(f"  arrival skew per tile (max-min over the 8 waves): median {med(skew):.0f}, p90 {float(np.percentile(skew, 90)):.0f}")
+    start_skew = t0.max(1) - t0.min(1)
+    print(f"  workgroup start skew {med(start_skew):.0f}; workgroups' start spread {float(t0[:, 0].max() - t0[:, 0].min()):.0f}")
+
+
+if __name__ == "__main__":
+    main()
