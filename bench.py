@@ -31,38 +31,82 @@ MFMA_PEAK_BF16_TFLOPS = 2500.0   # dense, MI355X_MICROARCH.md:43
 MFMA_PEAK_F32_TFLOPS = 157.3
 
 
-class DominantKernelTimer:
-    """HIP events around every launch of the dominant kernel, on the launch stream."""
+HBM_PEAK_GBPS = 8000.0          # spec, MI355X_MICROARCH.md:36 (6.29 TB/s measured copy)
+
+
+class LaunchTimer:
+    """HIP events around the launches of interest, on the launch stream (torch's current stream,
+    which the binding launches on): the dominant kernel (G1/G7 self-attention, FLOP) and the
+    HBM-bound map-store launches (the G2/G6 cross-attention calls that keep their maps, and under
+    --store-self the G2/G6 self calls whose maps kept: fused pass + self_maps_kernel), with their
+    algorithmic bytes."""
 
     def __init__(self, n_query=4096):
         self.n_query = n_query
-        self.pairs = []
-        self.flops = []
+        self.rec = {}            # name -> list of (start event, end event, work)
         self._pending = None
         self.enabled = False
 
-    def before(self, kind, t):
-        if self.enabled and kind == "self" and t.n_query == self.n_query:
+    @staticmethod
+    def _bytes(kind, t, info):
+        """Algorithmic HBM bytes of one launch: q, k, v read once, o written once (bf16 or f32),
+        and the kept maps: f32 [stored * H, P, K] written on the first step, read + written after."""
+        es = 2 if t.io_dtype == 1 else 4
+        C = t.n_heads * t.head_dim
+        io = es * t.n_batch * C * (2 * t.n_query + 2 * t.n_key)
+        maps = 4.0 * info["stored"] * t.n_heads * t.n_query * t.n_key * (2 if info["accumulate"] else 1)
+        return io + maps
+
+    def _name(self, kind, t, info):
+        if kind == "self" and t.n_query == self.n_query and info["stored"] == 0:
+            return "dominant"
+        if t.n_query == 1024 and info["stored"] > 0 and info["accumulate"]:
+            return f"{kind}_store_p1024"
+        return None
+
+    def before(self, kind, t, info=None):
+        info = info or {"stored": 0, "accumulate": False}
+        name = self._name(kind, t, info) if self.enabled else None
+        if name is not None:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self._pending = (ev, 4.0 * t.n_query * t.n_key * t.n_heads * t.head_dim * t.n_batch)
+            work = (4.0 * t.n_query * t.n_key * t.n_heads * t.head_dim * t.n_batch if name == "dominant"
+                    else self._bytes(kind, t, info))
+            self._pending = (name, ev, work)
 
-    def after(self, kind, t):
+    def after(self, kind, t, info=None):
         if self._pending is not None:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self.pairs.append((self._pending[0], ev))
-            self.flops.append(self._pending[1])
+            name, start, work = self._pending
+            self.rec.setdefault(name, []).append((start, ev, work))
             self._pending = None
 
-    def summary(self):
+    def summary(self, name="dominant"):
+        """(average ms per launch, average work per launch, launches)"""
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b in self.pairs]
-        if not ms:
+        pairs = self.rec.get(name, [])
+        if not pairs:
             return None, None, 0
-        avg_ms = sum(ms) / len(ms)
-        flops = sum(self.flops) / len(self.flops)
-        return avg_ms, flops, len(ms)
+        ms = [a.elapsed_time(b) for a, b, _ in pairs]
+        return sum(ms) / len(ms), sum(w for _, _, w in pairs) / len(pairs), len(ms)
+
+    def hbm_lines(self):
+        out = []
+        labels = {"cross_store_p1024": "cross_attn_kernel G2/G6 (P=1024, d=80, K=77) with the kept cross maps "
+                                       "(read-add-write) + LocalBlend word sums",
+                  "self_store_p1024": "self-attention G2/G6 (P=K=1024, d=80) with the kept self maps: fused "
+                                      "pass (lse) + self_maps_kernel read-add-write"}
+        for name in ("cross_store_p1024", "self_store_p1024"):
+            avg_ms, nbytes, n = self.summary(name)
+            if not n:
+                continue
+            gbps = nbytes / (avg_ms * 1e-3) / 1e9
+            out.append({"kernel": labels[name], "avg_launch_ms": avg_ms, "launches": n,
+                        "algorithmic_bytes": nbytes, "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": gbps / HBM_PEAK_GBPS,
+                        "bytes_rule": "q + o + k + v (io dtype) + kept maps f32 x2 (read + write, steps >= 1)"})
+        return out
 
 
 def pmc_traffic():
@@ -176,7 +220,7 @@ def main():
     model = pl.SyntheticStableDiffusion(device=dev, dtype=dtype)
     prompts = pl.north_star_prompts()
     B = len(prompts)
-    timer = DominantKernelTimer()
+    timer = LaunchTimer()
     _hip.LAUNCH_OBSERVER = timer
 
     G = args.groups_per_call
@@ -247,7 +291,8 @@ def main():
                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                     "algorithmic_bytes": 4.0 * 8 * G * 4096 * 320 * 2,
-                    "kernel": f"self_attn_multi_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 2 x 32 queries per wave, 256-key tiles, pipelined sub-blocks)",
+                    "kernel": f"self40_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 8 waves x 2 x 32 queries, "
+                              f"256-key tiles, software-pipelined 32x32 blocks)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops}
         cpu = None
@@ -268,6 +313,9 @@ def main():
                        "self_maps_kept": args.store_self, "gathered": "final latents + 16x16 cross maps (1 all-gather)",
                        "parallelism": f"replicas x{world} (groups by seed)"},
             "roofline": roofline, "cpu_baseline": cpu,
+            # the HBM-bound launches of the path (north star: "achieved HBM GB/s for the map and blend
+            # kernels"), HIP-event timed in the same run; algorithmic bytes, not PMC
+            "roofline_hbm": timer.hbm_lines(),
         }
         print(json.dumps(line))
     if world > 1:

@@ -586,7 +586,10 @@ int run_self40(const SelfArgs& a, hipStream_t st) {
     case 82: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // split + alternate every 4 steps
     case 83: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // 81 with clock stamps
 #endif
-    default: return (int)launch<8, 2, 256, true, 1>(a, st);
+    case 66: return (int)launch<8, 2, 256, true, 1>(a, st);   // round-3 first LEAN default
+    // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
+    // alternate step pairs: G1 0.1931-0.1938 ms vs 0.1964 (66) and 0.2056 (round 2), profiles/r03
+    default: return (int)launch<8, 2, 256, true, 1 | 128 | 256>(a, st);
   }
 #endif
 }

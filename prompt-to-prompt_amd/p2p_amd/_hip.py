@@ -18,8 +18,9 @@ if os.environ.get("P2P_EXPERIMENTS_LIB") == "1":
     _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "exp", "libp2p_hip.so")
 _lib = None
 
-# Optional launch observer (bench.py times the dominant kernel with HIP events through it):
-# an object with before(kind, tensors) / after(kind, tensors), called around each launch.
+# Optional launch observer (bench.py times the dominant kernel and the map-store launches with HIP
+# events through it): an object with before(kind, tensors, info) / after(kind, tensors, info),
+# called around each launch; info = {"stored": entries whose maps are kept, "accumulate": bool}.
 LAUNCH_OBSERVER = None
 
 P2P_DTYPE_F32 = 0
@@ -221,11 +222,13 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
         ws = _lse_workspace(q.device, t.n_batch * t.n_heads * t.n_query).data_ptr()
     obs = LAUNCH_OBSERVER
     if obs is not None:
-        obs.before("self", t)
+        info = {"stored": sum(1 for x in store_slot if int(x) >= 0) if ws is not None else 0,
+                "accumulate": bool(accumulate)}
+        obs.before("self", t, info)
     rc = lib().p2p_self_attn_fwd(ctypes.byref(t), src, store.data_ptr() if store is not None else None,
                                  slots, int(bool(accumulate)), ws, _stream(q.device))
     if obs is not None:
-        obs.after("self", t)
+        obs.after("self", t, info)
     _check(rc, "p2p_self_attn_fwd")
 
 
@@ -259,12 +262,14 @@ def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, sto
         assert store.dtype == torch.float32 and store.is_contiguous()
     obs = LAUNCH_OBSERVER
     if obs is not None:
-        obs.before("cross", t)
+        info = {"stored": sum(1 for x in store_slot if int(x) >= 0) if (store is not None and store_slot is not None)
+                else 0, "accumulate": bool(accumulate)}
+        obs.before("cross", t, info)
     rc = lib().p2p_cross_attn_fwd(ctypes.byref(t), G, len(groups),
                                   store.data_ptr() if store is not None else None, slots,
                                   int(bool(accumulate)), _stream(q.device))
     if obs is not None:
-        obs.after("cross", t)
+        obs.after("cross", t, info)
     _check(rc, "p2p_cross_attn_fwd")
 
 
