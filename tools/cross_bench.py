@@ -82,10 +82,16 @@ def main(iters=50):
         plain = [(0, B, None, None), (B, B, None, None)]
         edit = [(0, B, None, None), (B, B, prog, alpha)]
         edit0 = [(0, B, None, None), (B, B, prog0, alpha)]
+        # LocalBlend word sums folded into the store epilogue (the 16x16 layers G3/G5 in the pipeline):
+        # [count, 2, lh, P] f32 running sums, alpha / substruct weights [count, K]
+        lh = 5 * H
+        bsums = torch.zeros(B, 2, lh, P, device="cuda")
+        balpha = torch.rand(B, K, device="cuda")
+        blend = [(0, B, None, None), (B, B, prog, alpha, (bsums, balpha, None, 0, lh))]
         r = {"geom": name, "P": P, "d": d}
         for tag, grp, st in (("plain", plain, None), ("edit", edit, None), ("edit_no_terms", edit0, None),
                              ("store", plain, store),
-                             ("edit+store", edit, store)):
+                             ("edit+store", edit, store), ("edit+store+blend", blend, store)):
             fn = lambda: _hip.cross_attn(q, k, v, o, H, d ** -0.5, grp, store=st,  # noqa: E731
                                          store_slot=slots if st is not None else None,
                                          accumulate=st is not None)
