@@ -210,7 +210,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from p2p_amd import _hip, config, controllers, sweep
+    from p2p_amd import _hip, config, sweep
     from p2p_amd import pipeline as pl
     config.set_compute(args.compute)
     _hip.lib()
@@ -225,24 +225,8 @@ def main():
 
     G = args.groups_per_call
 
-    def make_ctrl():
-        return pl.make_replace_controller(prompts, args.ddim_steps, device=dev, store_self_maps=args.store_self)
-
-    def batch(seeds):
-        """One step: len(seeds) <= G edit groups (each 1 source + 3 edits, its own seed), one U-Net
-        call per DDIM step.  Returns the final latents [g, B, 4, 64, 64] and each group's reduced
-        stored maps [g, B, 16, 16, 77] (aggregate_attention's 16x16 cross average per prompt)."""
-        if len(seeds) == 1:
-            ctrl = make_ctrl()
-            lat = pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(seeds[0]), num_steps=args.ddim_steps)
-            maps = controllers.reduce_maps(ctrl, 16, ["up", "down"], True, B)
-            return lat[None], maps[None]
-        members = [make_ctrl() for _ in seeds]
-        ctrl = controllers.GroupBatch(members)
-        lat = pl.run_edit_groups(model, [prompts] * len(seeds), ctrl, [pl.seed_latent(s) for s in seeds],
-                                 num_steps=args.ddim_steps)
-        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in members])
-        return lat.reshape(len(seeds), B, *lat.shape[1:]), maps
+    # one step = one batch of G groups: the runner the configs[3] GPU test drives through the same sweep
+    batch = pl.sweep_batch_runner(model, prompts, args.ddim_steps, store_self_maps=args.store_self, device=dev)
 
     # groups (seeds) partitioned across ranks round-robin: no collective on the data path
     if args.seeds > 0:
@@ -265,7 +249,7 @@ def main():
 
     # the sweep tests/test_distributed.py runs over gloo: this rank's batches, then ONE RCCL
     # all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
-    lat_all, maps_all = sweep.run_batched_sweep(all_seeds, batch, [(B, 4, 64, 64), (B, 16, 16, 77)], rank, world, G,
+    lat_all, maps_all = sweep.run_batched_sweep(all_seeds, batch, batch.out_shapes, rank, world, G,
                                                 device=dev, on_batch=progress)
     torch.cuda.synchronize(dev)
     if world > 1:

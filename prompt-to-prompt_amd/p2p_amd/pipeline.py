@@ -136,6 +136,35 @@ def run_edit_groups(model: SyntheticStableDiffusion, prompt_groups: Sequence[Seq
     return latents
 
 
+def sweep_batch_runner(model: SyntheticStableDiffusion, prompts: Sequence[str], num_steps: int = 50,
+                       store_self_maps: bool = False, device=None):
+    """The unit of work bench.py times and the configs[3] sweep runs (sweep.run_batched_sweep):
+    run(seeds) denoises len(seeds) edit groups -- each 1 source + 3 AttentionReplace edits with
+    LocalBlend and its own seed -- one U-Net call per DDIM step (controllers.GroupBatch when
+    len(seeds) > 1), and returns the final latents [g, B, 4, 64, 64] and each group's reduced
+    stored maps [g, B, 16, 16, 77] (aggregate_attention's 16x16 cross average per prompt,
+    main.py:293-307)."""
+    from . import controllers
+    B = len(prompts)
+
+    def make_ctrl():
+        return make_replace_controller(prompts, num_steps, device=device, store_self_maps=store_self_maps)
+
+    def run(seeds):
+        if len(seeds) == 1:
+            ctrl = make_ctrl()
+            lat = run_edit_group(model, prompts, ctrl, seed_latent(seeds[0]), num_steps=num_steps)
+            return lat[None], controllers.reduce_maps(ctrl, 16, ["up", "down"], True, B)[None]
+        members = [make_ctrl() for _ in seeds]
+        lat = run_edit_groups(model, [prompts] * len(seeds), controllers.GroupBatch(members),
+                              [seed_latent(s) for s in seeds], num_steps=num_steps)
+        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in members])
+        return lat.reshape(len(seeds), B, *lat.shape[1:]), maps
+
+    run.out_shapes = [(B, 4, 64, 64), (B, 16, 16, 77)]
+    return run
+
+
 # BASELINE.json configs[2]: AttentionRefine + AttentionReweight (equalizer) groups whose 16/32-res
 # cross maps are all stored.  Each group refines the source prompt by inserted words and
 # reweights one word of it.

@@ -7,9 +7,9 @@
   math is fp32).  Bars (north star): final latents cosine >= 0.999 per prompt, LocalBlend masks
   agreeing on >= 99.9 % of the pixels.
 * configs[2] at its stated size: a batch of 8 Refine+Reweight edit groups (GroupBatch, one U-Net
-  call of batch 64 per step), each group against its own single-group ORACLE run: latents cosine
+  call of batch 64 per step), groups against their own single-group ORACLE runs: latents cosine
   >= 0.999 and every stored 16/32-res cross map within 2e-3 per accumulated step
-  (main.py:205, :233-278).
+  (main.py:205, :233-278) -- at the full 50 DDIM steps (f32 U-Net) and at 10 steps for all groups.
 """
 import pytest
 import torch
@@ -82,27 +82,28 @@ def test_bench_default_config_50_steps(cuda, tok):
 STEPS2 = 10
 
 
-@pytest.mark.parametrize("unet_dtype", [torch.float32, torch.bfloat16], ids=["f32unet", "bf16unet"])
-def test_config2_eight_refine_reweight_groups_vs_oracle(cuda, tok, unet_dtype):
+def _config2_vs_oracle(cuda, tok, unet_dtype, steps, check_groups, per_step_bar):
+    """A GroupBatch of 8 Refine+Reweight groups (one U-Net call of batch 64 per step) for `steps`
+    DDIM steps; the groups in check_groups each against their own single-group oracle run."""
     prompts = [pl.REFINE_SOURCE] + pl.REFINE_EDITS
     seeds = list(range(20, 28))
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=unet_dtype)
     with config.compute_mode("bf16"):
-        members = [pl.make_refine_reweight_controller(prompts, STEPS2, device=cuda, tokenizer=tok) for _ in seeds]
+        members = [pl.make_refine_reweight_controller(prompts, steps, device=cuda, tokenizer=tok) for _ in seeds]
         batch = controllers.GroupBatch(members)
         got = pl.run_edit_groups(model, [prompts] * len(seeds), batch, [pl.seed_latent(s) for s in seeds],
-                                 num_steps=STEPS2)
+                                 num_steps=steps)
     torch.cuda.synchronize()
-    print(f"product GroupBatch of {len(seeds)} groups done", flush=True)
+    print(f"product GroupBatch of {len(seeds)} groups x {steps} steps done", flush=True)
     B = len(prompts)
     worst_cos, worst_map = 1.0, 0.0
-    for g, s in enumerate(seeds):
-        octrl = oracle_controller("refine_reweight", prompts, tok, STEPS2, cuda)
-        want = oracle_group(model, prompts, pl.seed_latent(s), octrl, STEPS2)
+    for g in check_groups:
+        octrl = oracle_controller("refine_reweight", prompts, tok, steps, cuda)
+        want = oracle_group(model, prompts, pl.seed_latent(seeds[g]), octrl, steps)
         cos = cosine(got[g * B:(g + 1) * B], want)
         worst_cos = min(worst_cos, cos.min().item())
         m = members[g]
-        assert m.cur_step == octrl.cur_step == STEPS2
+        assert m.cur_step == octrl.cur_step == steps
         for key in ("down_cross", "mid_cross", "up_cross"):
             ours, ref = m.attention_store[key], octrl.attention_store[key]
             assert len(ours) == len(ref), key
@@ -110,13 +111,27 @@ def test_config2_eight_refine_reweight_groups_vs_oracle(cuda, tok, unet_dtype):
                 worst_map = max(worst_map, (x - y).abs().max().item())
         assert m.attention_store["down_self"] == [] and octrl.attention_store["down_self"] == []
         print(f"  group {g}: cosine {cos.min().item():.6f}", flush=True)
-    print(f"configs[2] 8 groups x {STEPS2} steps ({unet_dtype}): worst latent cosine {worst_cos:.6f}, "
-          f"worst stored cross-map |diff| {worst_map:.3e}")
+    print(f"configs[2] 8 groups x {steps} steps ({unet_dtype}), oracle groups {list(check_groups)}: worst latent "
+          f"cosine {worst_cos:.6f}, worst stored cross-map |diff| {worst_map:.3e} "
+          f"({worst_map / steps:.2e} per accumulated step)")
     assert worst_cos >= 0.999
-    # bf16 kernels on identical inputs: the north-star 2e-3 per accumulated step (f32 U-Net: both
-    # runs see the same q/k up to the attention's own rounding).  With the bf16 U-Net the oracle's
-    # fp32 attention sends its OWN bf16 activations down a slightly different path, so the maps are
-    # compared across two U-Net trajectories (measured 2.3e-3 per step; the kernel error on the
-    # same inputs is pinned per call in test_gpu_controllers.py::test_edits_bf16_sd_geometry[*bf16in])
-    bar = (2e-3 if unet_dtype == torch.float32 else 3e-3) * STEPS2
-    assert worst_map < bar
+    assert worst_map < per_step_bar * steps
+
+
+def test_config2_f32unet_50_steps_vs_oracle(cuda, tok):
+    """configs[2] at its stated schedule (50 DDIM steps), f32 U-Net: both runs see the same q/k up
+    to the attention's own rounding, so every stored 16/32-res cross map stays within the
+    north-star 2e-3 per accumulated step.  Two of the eight groups (first and last of the batch)
+    are checked against single-group oracle runs (an oracle group costs ~50 fp32 eager U-Net
+    calls); all eight at 10 steps below."""
+    _config2_vs_oracle(cuda, tok, torch.float32, 50, (0, 7), 2e-3)
+
+
+@pytest.mark.parametrize("unet_dtype", [torch.float32, torch.bfloat16], ids=["f32unet", "bf16unet"])
+def test_config2_eight_refine_reweight_groups_vs_oracle(cuda, tok, unet_dtype):
+    """All eight groups at 10 steps.  bf16 U-Net: the oracle's fp32 attention sends its OWN bf16
+    activations down a slightly different path, so the maps are compared across two U-Net
+    trajectories (measured 2.1e-3 per step; the kernel error on identical inputs is pinned per call
+    in test_gpu_controllers.py::test_edits_bf16_sd_geometry[*bf16in]) -- 3e-3 there, 2e-3 with the
+    f32 U-Net."""
+    _config2_vs_oracle(cuda, tok, unet_dtype, STEPS2, range(8), 2e-3 if unet_dtype == torch.float32 else 3e-3)

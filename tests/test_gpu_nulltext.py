@@ -60,15 +60,16 @@ def test_null_text_inversion_matches_oracle(cuda, use_graphs):
         print(f"step {i}: |update| {d_want.norm().item():.4f}, cos(updates) {cos(d_prod, d_want):.5f}, "
               f"cos(embeddings) {cos(e, w):.7f}")
         assert cos(e, w) >= 0.9999
-        assert cos(d_prod, d_want) >= 0.95
+        assert cos(d_prod, d_want) >= 0.998     # measured >= 0.99946 (profiles/r02b, r03)
 
 
 def test_null_text_inversion_full_schedule(cuda):
     """configs[4] at its stated schedule: 50 DDIM steps x 10 Adam steps (null_text.py:591-618,
     early stop 1e-5), graphed product path vs the oracle's fp32 autograd on the same weights.  Over
-    50 dependent steps the bf16-kernel gradients drift, so the per-step bar is on the optimiser's
-    updates (cosine >= 0.9) and on the embeddings themselves (>= 0.999); the DDIM trajectory is a
-    forward-only quantity and stays at >= 0.9999."""
+    50 dependent steps the bf16-kernel gradients drift a little: the per-step bars are cosine >= 0.999
+    on the optimiser's updates and >= 0.9995 on the embeddings themselves (measured 0.9995 and 0.99967,
+    profiles/r02b/nulltext_full_schedule.log); the DDIM trajectory is a forward-only quantity and
+    stays at >= 0.9999."""
     steps, inner = 50, 10
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
     g = torch.Generator().manual_seed(7)
@@ -92,8 +93,8 @@ def test_null_text_inversion_full_schedule(cuda):
         if (w - u0).norm().item() > 1e-6:
             worst_u = min(worst_u, cos(e - u0, w - u0))
     print(f"50x10 null-text: worst cos(embeddings) {worst_e:.6f}, worst cos(updates) {worst_u:.4f}")
-    assert worst_e >= 0.999
-    assert worst_u >= 0.9
+    assert worst_e >= 0.9995
+    assert worst_u >= 0.999
 
 
 def test_edit_with_null_embeddings(cuda, tok):

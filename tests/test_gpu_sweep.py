@@ -1,0 +1,56 @@
+"""configs[3] on a GPU: the seed sweep exactly as bench.py --seeds S --groups-per-call 8 times it
+(sweep.run_batched_sweep over pipeline.sweep_batch_runner; main.py:425-444 is the reference's
+sequential seed loop), at world size 1 on the box's single GPU.  The multi-rank partition + gather
+of the same function runs over gloo in tests/test_distributed.py.
+
+16 seeds in batches of 8 groups per U-Net call (bf16 U-Net, bf16 kernels, 50 DDIM steps, 1 source
++ 3 AttentionReplace edits + LocalBlend per group).  Two sampled groups -- one from each batch --
+against single-group ORACLE runs on the same weights (fp32 eager attention + reference controller
++ LocalBlend + DDIM): final latents cosine >= 0.999 per prompt and the gathered 16x16 cross maps
+within 3e-3 (two bf16-U-Net trajectories; test_gpu_bench_config.py); every source prompt's
+gathered map row sums to 1.
+"""
+import pytest
+import torch
+
+from oracle import control as oc
+from oracle_runs import cosine, oracle_controller, oracle_group
+from p2p_amd import config, controllers, sweep
+from p2p_amd import pipeline as pl
+
+pytestmark = pytest.mark.gpu
+
+SEEDS, GPC, STEPS = 16, 8, 50
+
+
+def test_config3_sweep_world1_vs_oracle(cuda, tok):
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    prompts = pl.north_star_prompts()
+    B = len(prompts)
+    run = pl.sweep_batch_runner(model, prompts, STEPS, device=cuda)
+    seeds = list(range(SEEDS))
+    done = []
+    with config.compute_mode("bf16"):
+        lat, maps = sweep.run_batched_sweep(seeds, run, run.out_shapes, rank=0, world=1, groups_per_call=GPC,
+                                            device=cuda, on_batch=lambda i, n: done.append(i))
+    torch.cuda.synchronize()
+    assert done == [0, 1]
+    assert lat.shape == (SEEDS, B, 4, 64, 64) and maps.shape == (SEEDS, B, 16, 16, 77)
+    assert torch.isfinite(lat).all() and torch.isfinite(maps).all()
+    row_err = (maps[:, 0].sum(-1) - 1).abs().max().item()
+    print(f"configs[3] sweep: {SEEDS} groups, source map rows sum to 1 within {row_err:.2e}", flush=True)
+    assert row_err < 1e-3
+    for s in (3, 12):
+        lb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok)
+        lb.alpha = lb.alpha.to(cuda)
+        octrl = oracle_controller("replace", prompts, tok, STEPS, cuda, local_blend=lb)
+        want = oracle_group(model, prompts, pl.seed_latent(s), octrl, STEPS)
+        cos = cosine(lat[s], want)
+        store = controllers.AttentionStore()            # the product's reduction over the oracle's store
+        store.attention_store, store.cur_step = octrl.attention_store, octrl.cur_step
+        want_maps = controllers.reduce_maps(store, 16, ["up", "down"], True, B)
+        dmap = (maps[s] - want_maps).abs().max().item()
+        print(f"  seed {s}: latent cosine per prompt {[round(c, 6) for c in cos.tolist()]}, "
+              f"16x16 map |diff| {dmap:.2e}", flush=True)
+        assert cos.min().item() >= 0.999, cos
+        assert dmap < 3e-3
