@@ -1041,6 +1041,17 @@ __global__ __launch_bounds__(256) void self_probs_kernel(SelfArgs a, int kw) {
 // Stored maps leave through the same slab as whole contiguous rows (one [32, K] block per
 // wave).  The slab is dynamic LDS, allocated only by launches with an edit or a store, so a
 // plain launch runs at the occupancy of its K/V tiles alone.
+#ifdef P2P_EXPERIMENTS
+// diagnostic clock stamps of the cross kernel (experiments build, P2P_SELF_VARIANT 90):
+// [logical workgroup < 4096][wave < 4][slot < 16]; read back by p2p_diag_cross_stamps
+__device__ unsigned long long g_cross_stamps[4096 * 4 * 16];
+#define P2P_CROSS_STAMP(i)                                                                              \
+  if (a.variant == 90 && logical < 4096 && wave < 4 && lane == 0)                                       \
+    g_cross_stamps[(logical * 4 + wave) * 16 + (i)] = __builtin_amdgcn_s_memtime();
+#else
+#define P2P_CROSS_STAMP(i)
+#endif
+
 template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
 __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
@@ -1071,15 +1082,27 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   const int qi = lane & 31;
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  P2P_CROSS_STAMP(0)
+  // Kernel arguments live in memory: every a.field is a scalar load, and a chain of dependent
+  // ones costs a round trip each at the start of every workgroup.  Everything the lean path reads
+  // that does not depend on the entry is pinned here, so it all arrives in ONE round trip; the
+  // entry's packed info is the one dependent load after it.
+  asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.N), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v),
+               "s"(a.o), "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv),
+               "s"(a.bso), "s"(a.scale_log2));
   const int qt = logical % a.n_qtiles;
   const int rest = logical / a.n_qtiles;
   const int h = rest % a.H;
   const int n = a.N - 1 - rest / a.H;  // the edits sit last in the batch: dispatch them first
-  const int gi = a.ent_group[n];
-  const int first = a.grp_first[gi];
-  const int b = n - first;
-  const char* const prog = static_cast<const char*>(a.grp_prog[gi]);
-  const bool edit = prog != nullptr && b > 0;
+  // one dependent kernel-argument load decides the path (every a.field read is a scalar memory
+  // round trip; chains of them cost ~1 us at the start of every workgroup)
+  const int info = a.ent_info[n];
+  asm volatile("" ::"s"(info));
+  const int gi = info & 0xff;
+  const int b = (info >> 8) & 0xff;
+  const int first = n - b;
+  const bool edit = (info >> 16) & 1;
+  const bool stored = (info >> 17) & 1;
   const int p0w = qt * 32 * WAVES + wave * 32;
   const int p = p0w + qi;
   const bool prow = p < a.P;
@@ -1094,7 +1117,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   // (no per-element sum, no normalised P: O is scaled once); only a key block that runs past K
   // is masked.  (Measured at G1, N = 8, H = 8: tools/cross_bench.py, profiles/r02.)
   if constexpr (MP::kElemBytes == 2 && DV > D) {
-    if (!edit && !(a.store && a.store_slot[n] >= 0)) {
+    if (!edit && !stored) {
       constexpr int kLdt = D / 32;
       constexpr int kLrr = D % 32;
       constexpr int kLh = (kLrr >> 2) & 1;
@@ -1121,6 +1144,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
           vc[i].load(vp + (int64_t)row * a.ldv + ch * 8);
         }
       }
+      P2P_CROSS_STAMP(1)
       if constexpr (DK > D) {   // K columns D..DK of every row: Q's zero columns meet zeros, not stale LDS
         constexpr int PC = (DK - D) / 8;
         for (int i = tid; i < KR * PC * MQ::planes; i += NT) {
@@ -1143,6 +1167,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
         }
       }
       __syncthreads();
+      P2P_CROSS_STAMP(2)
       float sv[KB][16];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
@@ -1178,11 +1203,13 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       };
       if (K <= (KB - 1) * 32 + 16) soft(std::true_type{});
       else soft(std::false_type{});
+      P2P_CROSS_STAMP(3)
       f32x16_t O[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
+      P2P_CROSS_STAMP(4)
       const float inv = 1.f / __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
       if (prow) {
         IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
@@ -1196,8 +1223,43 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
                      O[dt][4 * g + 3] * inv);
           }
       }
+      P2P_CROSS_STAMP(5)
       return;
     }
+  }
+
+  const char* const prog = static_cast<const char*>(a.grp_prog[gi]);
+  const int slot = a.store_slot[n];
+  // maps kept and accumulated: touch this wave's rows of the running sum now (32 x K f32,
+  // contiguous), so the read-add-write of the store epilogue finds them in this XCD's L2 instead of
+  // paying an HBM round trip at the end of the workgroup
+  // (two loads per lane cover 32 rows of up to 96 keys; their values are only consumed at the very
+  // end, so nothing waits for them)
+  float touch0 = 0.f, touch1 = 0.f;
+  if (stored && a.store_accumulate) {
+    const int rows = min(32, a.P - p0w);
+    const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
+    const int lines = (rows * K * 4 + 127) / 128;
+    static_assert(32 * P2P_MAX_KEYS_CROSS * 4 / 128 <= 128, "two touches per lane");
+    if (lane < lines) touch0 = g[lane * 32];
+    if (lane + 64 < lines) touch1 = g[(lane + 64) * 32];
+  }
+  // LocalBlend word weights of this entry (lanes 0-31: alpha, 32-63: substruct) into LDS now; the
+  // store epilogue's per-row word sums then read them from LDS, not global memory
+  __shared__ float btab[2][P2P_MAX_KEYS_CROSS];
+  const bool blend_on = stored && a.grp_bsum[gi] != nullptr;
+  if (blend_on) {
+    const float* const ta = a.grp_balpha[gi] + (int64_t)b * K;
+    const float* const tsub = a.grp_bsub[gi];
+    static_assert(2 * P2P_MAX_KEYS_CROSS <= 2 * NT, "two weights per thread");
+    float w0 = 0.f, w1 = 0.f;
+    const int i1 = tid + NT;
+    if (tid < K) w0 = ta[tid];
+    else if (tid < 2 * K && tsub != nullptr) w0 = tsub[(int64_t)b * K + tid - K];
+    if (i1 < K) w1 = ta[i1];
+    else if (i1 < 2 * K && tsub != nullptr) w1 = tsub[(int64_t)b * K + i1 - K];
+    if (tid < 2 * K) btab[tid < K ? 0 : 1][tid < K ? tid : tid - K] = w0;
+    if (i1 < 2 * K) btab[i1 < K ? 0 : 1][i1 < K ? i1 : i1 - K] = w1;
   }
 
   // padding the MFMAs read but the staging never writes (disjoint from it: no extra barrier):
@@ -1317,30 +1379,53 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   f32x16_t Rd[KB];
   if constexpr (kDenseOk) {
    if (dense) {
-    const int* hdr = reinterpret_cast<const int*>(prog);
-    const uint16_t* mg = reinterpret_cast<const uint16_t*>(prog + hdr[5]) +
+    const uint16_t* mg = static_cast<const uint16_t*>(a.grp_dense[gi]) +
                          (int64_t)(b - 1) * P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE;
     EV* const Ms = reinterpret_cast<EV*>(cross_dyn);  // [96 source words][96 target words]
+    // every global load of the prologue first (mapper tile chunks, coefficients, the source's Q
+    // and K), then the LDS writes: one memory round trip instead of a chain of them
+    constexpr int kMCh = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE / 8;   // 16-byte chunks of the tile
+    constexpr int kMPer = (kMCh + NT - 1) / NT;
+    short8_t mreg[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      const int i = tid + j * NT;
+      if (i < kMCh) mreg[j] = reinterpret_cast<const short8_t*>(mg)[i];
+    }
+    const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
+                                                     (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES);
+    const float* al = a.grp_alpha[gi] + (b - 1) * K;
+    static_assert(KR <= NT, "one column per thread");
+    const int w = tid;
+    float aw = 0.f, cw = 0.f, pw = 0.f;
+    if (w < K) {
+      aw = al[w];
+      cw = ce[w];
+      pw = ce[P2P_PROGRAM_COLS + w];
+    }
+    Chunk8<IO> kc0[NCH], vc0[NCH];
+    load_kv(first, kc0, vc0, false);
     load_q(first, qf);
-    for (int i = tid; i < P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE / 8; i += NT)
-      reinterpret_cast<short8_t*>(Ms)[i] = reinterpret_cast<const short8_t*>(mg)[i];
-    {  // per-column c_rep / post / alpha next to the tile, read back after the barriers
-      const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
-                                                       (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES);
-      const float* al = a.grp_alpha[gi] + (b - 1) * K;
-      // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B: two coefficients per column
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      const int i = tid + j * NT;
+      if (i < kMCh) reinterpret_cast<short8_t*>(Ms)[i] = mreg[j];
+    }
+    {  // per-column coefficients next to the tile, read back after the barriers:
+      // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B
       float* col = reinterpret_cast<float*>(cross_dyn + kDenseTile);
-      for (int w = tid; w < KR; w += NT) {
-        const float aw = w < K ? al[w] : 0.f;
-        const float ap = aw * ce[P2P_PROGRAM_COLS + w];
-        col[w] = fmaf(ap, ce[w], 1.f - aw);
+      if (w < KR) {
+        const float ap = aw * pw;
+        col[w] = fmaf(ap, cw, 1.f - aw);
         col[KR + w] = ap;
       }
     }
-    stage(first, false);
+    store_kv(kc0, vc0, false);
     __syncthreads();
+    P2P_CROSS_STAMP(8)
     float p0[KB][16];
     probs(qf, p0);
+    P2P_CROSS_STAMP(9)
     load_q(n, qf);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) Rd[kb] = f32x16_t{};
@@ -1366,6 +1451,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       }
     }
     __syncthreads();  // every wave is done with the source K tile and the mapper tile
+    P2P_CROSS_STAMP(10)
    }
   }
   if (edit && !dense) {
@@ -1388,7 +1474,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   }
   stage(n, true);
   __syncthreads();
+  P2P_CROSS_STAMP(11)
   probs(qf, sv);
+  P2P_CROSS_STAMP(12)
 
   if (dense) {
     // a lane's columns come in runs of 4 (r & 3): one 16-byte LDS read per run and table;
@@ -1446,9 +1534,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       }
   }
 
+  P2P_CROSS_STAMP(13)
   // ---- AttentionStore epilogue: post-edit maps, whole rows through the wave's slab
-  const int slot = a.store_slot[n];
-  if (a.store && slot >= 0) {
+  if (stored) {
     __syncthreads();  // every lane of the wave is done gathering from the slab
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
@@ -1461,11 +1549,10 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     const int rows = min(32, a.P - p0w);
     // LocalBlend's word sums of these rows (lanes 0-31: alpha, 32-63: substruct), folded here so
     // the blend never re-reads the maps; words summed in index order as blend_wordsum_kernel does
-    if (a.grp_bsum[gi] != nullptr && qi < rows) {
-      const float* tab = hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi];
+    if (blend_on && qi < rows) {
       float acc = 0.f;
-      if (tab != nullptr) {
-        tab += (int64_t)b * K;
+      if ((hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi]) != nullptr) {
+        const float* tab = btab[hh];
         const float* row = slab + qi * K;
         for (int w = 0; w < K; ++w) acc += row[w] * tab[w];
       }
@@ -1493,18 +1580,22 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
           const int i = lane + 64 * j;
           if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
         }
+        // keeps the prefetch touches alive (never true: a running sum of probabilities is finite)
+        if (__builtin_expect(touch0 == -INFINITY || touch1 == -INFINITY, 0)) g[0] = touch0 + touch1;
       } else {
         for (int i = lane; i < count; i += 64) g[i] = a.store_accumulate ? g[i] + slab[i] : slab[i];
       }
     }
   }
 
+  P2P_CROSS_STAMP(14)
   // ---- O = P' V
   f32x16_t O[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
+  P2P_CROSS_STAMP(15)
   if (prow) {
     IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
 #pragma unroll
@@ -1783,3 +1874,16 @@ int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t 
 }
 
 }  // namespace p2p
+
+#ifdef P2P_EXPERIMENTS
+// dst == nullptr: clear the stamps
+extern "C" int p2p_diag_cross_stamps(void* dst, int64_t bytes) {
+  const int64_t n = (int64_t)sizeof(p2p::g_cross_stamps);
+  if (dst == nullptr) {
+    void* p = nullptr;
+    hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(p2p::g_cross_stamps));
+    return e != hipSuccess ? (int)e : (int)hipMemset(p, 0, n);
+  }
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(p2p::g_cross_stamps), bytes < n ? bytes : n, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -135,6 +135,11 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     a.grp_first[g] = G.first;
     a.grp_count[g] = G.count;
     a.grp_prog[g] = G.program;
+    // dense tiles follow the header and the n_edits records (programs.py layout)
+    a.grp_dense[g] = (G.program && (G.flags & P2P_PROGRAM_F_DENSE))
+                         ? static_cast<const char*>(G.program) + P2P_PROGRAM_HEADER_BYTES +
+                               (int64_t)G.n_edits * P2P_PROGRAM_REC_BYTES
+                         : nullptr;
     a.grp_alpha[g] = G.alpha;
     a.grp_flags[g] = G.program ? G.flags : 0;
     a.grp_bsum[g] = G.blend_sums;
@@ -162,6 +167,12 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     if (groups[g].blend_sums)
       for (int e = groups[g].first; e < groups[g].first + groups[g].count; ++e)
         if (a.store_slot[e] < 0) return P2P_E_ARG;
+  for (int n = 0; n < t->n_batch; ++n) {
+    const int g = a.ent_group[n];
+    const int b = n - a.grp_first[g];
+    const bool edit = a.grp_prog[g] != nullptr && b > 0;
+    a.ent_info[n] = g | (b << 8) | (edit ? 1 << 16 : 0) | (a.store_slot[n] >= 0 ? 1 << 17 : 0);
+  }
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;
   a.any_store = any_store ? 1 : 0;

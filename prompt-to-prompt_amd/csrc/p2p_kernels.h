@@ -50,9 +50,13 @@ struct CrossArgs {
   int variant;                   // launch-shape experiments (P2P_SELF_VARIANT, experiments build only)
   int store_slot[P2P_MAX_BATCH];
   int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
+  // per entry, packed so ONE kernel-argument load after n decides the path: group (bits 0-7),
+  // position in the group (8-15), edits (16), keeps its maps (17)
+  int ent_info[P2P_MAX_BATCH];
   int grp_first[P2P_MAX_GROUPS];
   int grp_count[P2P_MAX_GROUPS];
   const void* grp_prog[P2P_MAX_GROUPS];
+  const void* grp_dense[P2P_MAX_GROUPS];   // the program's dense f16 tiles (host-computed offset)
   const float* grp_alpha[P2P_MAX_GROUPS];
   int grp_flags[P2P_MAX_GROUPS];
   float* grp_bsum[P2P_MAX_GROUPS];         // LocalBlend word sums (p2p_group.blend_*)
