@@ -1653,7 +1653,7 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
       // bf16 inputs: the software-pipelined F16-form kernel (p2p_self40.hip); experiments
       // variants 40-45 select the round-2 multi-block kernel instead
       if constexpr (kF16)
-        if (self40_eligible(a) && (a.variant == 0 || a.variant >= 60)) return (hipError_t)run_self40(a, st);
+        if (self40_eligible(a, 40) && (a.variant == 0 || a.variant >= 60)) return (hipError_t)run_self40(a, 40, st);
       if (a.variant == 0 && a.P >= 2048) {
         // f32 inputs (split-bf16 Q K^T, two K planes): the multi-block kernel, 128-key tiles;
         // bf16 inputs with K < 256: the same with the F16 form
@@ -1686,6 +1686,13 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
       }
 #endif
     }
+  }
+  if constexpr (MP::kElemBytes == 2 && D == 80 && MQ::planes == 1 && sizeof(IO) == 2) {
+    // d = 80, bf16 inputs, nothing but O wanted (G2/G6 without kept maps or autograd): the
+    // software-pipelined kernel of p2p_self40.hip in its bf16 form
+    if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && self40_eligible(a, 80) &&
+        (a.variant == 0 || a.variant >= 91))
+      return (hipError_t)run_self40(a, 80, st);
   }
   if (mode == MODE_FUSED) {
     // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)

@@ -75,9 +75,10 @@ int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream
 // materialise protocol: probs (a.store) [N*H, P, K] = softmax(Q K^T * scale), optional key mask
 int run_self_probs(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
-// d = 40 self-attention with bf16 inputs, O only (p2p_self40.hip): the G1/G7 production kernel
-bool self40_eligible(const SelfArgs& a);
-int run_self40(const SelfArgs& a, hipStream_t st);
+// d = 40 / 80 self-attention with bf16 inputs, O only (p2p_self40.hip): the G1/G7 and G2/G6
+// production kernels
+bool self40_eligible(const SelfArgs& a, int d);
+int run_self40(const SelfArgs& a, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);
 

@@ -32,12 +32,27 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 
-constexpr int kD = 40;
-constexpr int kNKT = 3;    // 16-deep k steps of Q K^T (d padded to 48)
-constexpr int kNDT = 2;    // 32-row tiles of O^T (d padded to 64: rows 0-39 data, 40 row sums)
-constexpr int kKS = 56;    // f16 elements per K row in LDS: 112 B, a b128 read of 16 rows hits 16 slots
+// Head-dim geometry.  d = 40 (G1/G7): the F16 form (Q prescaled by c in f16, K staged as f16,
+// -m in the padding column 40 of the 48-deep Q K^T); d = 80 (G2/G6): the bf16 form (raw bf16 Q
+// and K, 5 k steps with no padding, p = exp2(fma(s, c, -m))).  O^T's row D is the row sum (V's
+// column D is 1).
+template <int D>
+struct Geom;
+template <>
+struct Geom<40> {
+  static constexpr bool F16 = true;
+  static constexpr int NKT = 3;    // 16-deep k steps of Q K^T (d padded to 48, column 40 = -m)
+  static constexpr int NDT = 2;    // 32-row tiles of O^T (rows 0-39 data, 40 row sums)
+  static constexpr int KS = 56;    // K row in LDS: 112 B, a b128 read of 16 rows hits 16 slots
+};
+template <>
+struct Geom<80> {
+  static constexpr bool F16 = false;
+  static constexpr int NKT = 5;
+  static constexpr int NDT = 3;    // rows 0-79 data, 80 row sums
+  static constexpr int KS = 88;    // 176 B: 16 rows of a b128 read on 16 distinct slots
+};
 constexpr int kVS = 96;    // bf16 elements per V row in LDS: 192 B, conflict-free transposed reads
-constexpr int kCPR = kD / 8;   // 16-byte chunks per K/V row
 
 template <int... I, typename F>
 __device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
@@ -69,8 +84,23 @@ __device__ unsigned long long g_s40_stamps[256 * 8 * kStampSlots];
 
 // One workgroup = WAVES waves x QB query blocks of 32 rows = 32*QB*WAVES queries of one (entry,
 // head); BK-key tiles, double-buffered in LDS.
-template <int WAVES, int QB, int BK, bool SCHED, int FORM>
-__global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(SelfArgs a) {
+template <int kD, int WAVES, int QB, int BK, bool SCHED, int FORM>
+// (FORM bit 4096: a 4-wave workgroup sized for two per CU -- two waves per SIMD, <= 256 VGPRs)
+__global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 : 1) void self40_kernel(SelfArgs a) {
+  using G = Geom<kD>;
+  constexpr bool kF16 = G::F16;
+  constexpr int kNKT = G::NKT;
+  constexpr int kNDT = G::NDT;
+  constexpr int kKS = G::KS;
+  constexpr int kCPR = kD / 8;   // 16-byte chunks per K/V row
+  constexpr int kDK = 16 * kNKT;
+  constexpr int kDV = 32 * kNDT;
+  static_assert(kDV > kD && (!kF16 || kDK > kD), "padding for the row-sum and -m columns");
+  // O^T row kD (the row sums): d tile kLdt, register kLr of the low lane half
+  constexpr int kLdt = kD / 32;
+  constexpr int kLrr = kD % 32;
+  constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+  static_assert(((kLrr >> 2) & 1) == 0, "the row sum sits in the low lane half");
   constexpr int NSB = BK / 32;
   constexpr int NT = 64 * WAVES;
   constexpr int NCH = (BK * kCPR + NT - 1) / NT;
@@ -83,16 +113,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   constexpr bool kSplit = (FORM & 128) != 0;
   constexpr int SCH = (BK * kCPR + NT / 2 - 1) / (NT / 2);   // chunks per thread, split staging
   constexpr int CMAX = kSplit ? SCH : NCH;
-  constexpr int kHalf = X / 2;  // staging writes start here, one chunk every spread(role) steps
+  // staging writes: chunk i of the next tile at step kHalf + i (X - kHalf) / n (several per step
+  // when there are more chunks than steps), from the middle of the tile on -- the loads issued at
+  // its start have landed by then
+  constexpr int kHalf = X / 2;
   auto nchunks = [](auto role) { return decltype(role)::value == 0 ? NCH : SCH; };
-  auto spread = [](auto role) {
-    constexpr int n = decltype(role)::value == 0 ? NCH : SCH;
-    return (X - kHalf) / n > 0 ? (X - kHalf) / n : 1;
-  };
-  static_assert(kHalf + (NCH - 1) * ((X - kHalf) / NCH > 0 ? (X - kHalf) / NCH : 1) < X, "chunks fit the tile");
-  static_assert(!kSplit || kHalf + (SCH - 1) * ((X - kHalf) / SCH > 0 ? (X - kHalf) / SCH : 1) < X, "chunks fit");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[2 * KBUF];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[2 * VBUF];
+  // K and V tile buffers; after the last tile the same LDS holds each wave's output rows (epilogue)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KBUF + 2 * VBUF];
+  uint16_t* const Ks = smem;
+  uint16_t* const Vs = smem + 2 * KBUF;
+  constexpr int kOS = kD + 8;   // output row in LDS: 16-byte aligned, rows on distinct banks
+  static_assert(WAVES * 32 * QB * kOS <= 2 * KBUF + 2 * VBUF, "epilogue rows fit the tile buffers");
   __shared__ int wg_flag;
 
   const int tid = threadIdx.x;
@@ -123,12 +154,15 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * kD;
   const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * kD;
 
-  // padding columns (written once; staging writes columns 0-39 only): K col 40 = f16 1.0 (the
-  // -m column), 41-47 = 0; V col 40 = bf16 1.0 (row sums), 41-63 = 0
+  // padding columns (written once; staging writes columns 0..D-1 only): F16 K column D = f16 1.0
+  // (the -m column), D+1..DK-1 = 0; V column D = bf16 1.0 (row sums), D+1..DV-1 = 0
   for (int r = tid; r < 2 * BK; r += NT) {
-    *reinterpret_cast<short8_t*>(Ks + r * kKS + kD) = short8_t{0x3C00, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < (kDK - kD) / 8; ++j)
+      *reinterpret_cast<short8_t*>(Ks + r * kKS + kD + 8 * j) =
+          short8_t{(short)(j == 0 && kF16 ? 0x3C00 : 0), 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < (kDV - kD) / 8; ++j)
       *reinterpret_cast<short8_t*>(Vs + r * kVS + kD + 8 * j) =
           short8_t{(short)(j == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
   }
@@ -159,10 +193,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
         qf[b][t] = v;
       }
   };
-  load_q(true);
-  // Q column 40 (k step 2, lane half 1, element 0) holds -m
+  load_q(kF16);
+  // F16: Q column D (k step D/16, lane half (D%16)/8, element D%8) holds -m
   auto set_mcol = [&](int b, float m) __attribute__((always_inline)) {
-    if (hh == 1) qf[b][2][0] = (short)__builtin_bit_cast(uint16_t, (_Float16)(-m));
+    if constexpr (kF16)
+      if (hh == (kD % 16) / 8) qf[b][kD / 16][kD % 8] = (short)__builtin_bit_cast(uint16_t, (_Float16)(-m));
   };
 
   // ---- K/V staging: chunk i of this thread = row cidx / 5, 16-byte chunk cidx % 5 (role 0: both
@@ -265,10 +300,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       for (int dt = 0; dt < kNDT; ++dt) vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
   };
 
-  stage_all(0, 0, true);
+  stage_all(0, 0, kF16);
   __syncthreads();
 
-  // ---- reference point: the row maximum of c s over the first 32 keys (Q column 40 is still 0)
+  // ---- reference point: the row maximum of c s over the first 32 keys (F16: Q column D is still 0)
   {
     short8_t kf[kNKT];
     read_k(Ks, 0, kf);
@@ -276,13 +311,17 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     for (int b = 0; b < QB; ++b) {
       f32x16_t acc = f32x16_t{};
 #pragma unroll
-      for (int t = 0; t < kNKT; ++t) mma_f16(acc, kf[t], qf[b][t]);
+      for (int t = 0; t < kNKT; ++t) {
+        if constexpr (kF16) mma_f16(acc, kf[t], qf[b][t]);
+        else mma_bf16(acc, kf[t], qf[b][t]);
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[r]);
       mx = fmaxf(mx, other_half(mx));
-      const float m = (float)(_Float16)mx;   // representable in Q's f16 column
-      ovf |= !(fabsf(m) < 65504.f);
+      if constexpr (!kF16) mx *= c;
+      const float m = kF16 ? (float)(_Float16)mx : mx;   // F16: representable in Q's f16 column
+      ovf |= !(fabsf(m) < (kF16 ? 65504.f : INFINITY));
       m_ref[b] = m;
       set_mcol(b, m);
     }
@@ -305,7 +344,6 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   auto tile = [&](int kt, auto more, auto masked, auto role) __attribute__((always_inline)) {
     constexpr bool kMore = decltype(more)::value;
     constexpr bool kMasked = decltype(masked)::value;
-    constexpr int kSpread = spread(role);
     constexpr int kNcw = nchunks(role);
     const int buf = kt & 1;
     if constexpr (kMore) stage_load(kt + 1, role);
@@ -328,7 +366,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       const int sb = x / QB, b = x % QB;
       S[x & 1] = f32x16_t{};
 #pragma unroll
-      for (int t = 0; t < kNKT; ++t) mma_f16(S[x & 1], kf[kslot(sb)][t], qf[b][t]);
+      for (int t = 0; t < kNKT; ++t) {
+        if constexpr (kF16) mma_f16(S[x & 1], kf[kslot(sb)][t], qf[b][t]);
+        else mma_bf16(S[x & 1], kf[kslot(sb)][t], qf[b][t]);
+      }
     };
     auto pv = [&](int x) __attribute__((always_inline)) {
       const int sb = x / QB, b = x % QB;
@@ -338,11 +379,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
         for (int dt = 0; dt < kNDT; ++dt) mma_bf16(O[b][dt], vf[vslot(sb)][s2][dt], pf[x & 1][s2]);
     };
     auto ex = [&](int x) __attribute__((always_inline)) {
-      const int sb = x / QB;
+      const int sb = x / QB, b = x % QB;
       float e[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float s = S[x & 1][r];
+        float s = kF16 ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
         if constexpr (kMasked)
           if (kt * BK + sb * 32 + acc_row(r, hh) >= K) s = -INFINITY;
         e[r] = fast_exp2(s);
@@ -370,21 +411,29 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
       constexpr int sb = x / QB, b = x % QB;
       // K of sub-block sb+1: LEAN after this step's Q K^T when it was the last one on sb
       // (b == QB-2: Q K^T of block x+1 = (sb, QB-1)), else early into the other slot
+      // (QB == 1: block x+1 is already on sb+1, so its K is read at the start of this step)
       constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSB;
+      constexpr bool kRdKEarly = kLeanK && kRdK && QB == 1;
       // V: LEAN reads V(sb) after this step's P V on block x-1 = (sb-1, QB-1); else V(sb+1) early
       constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSB);
       // the next tile's chunks go to the other buffer over the second half of the tile (every
       // wave has passed the barrier that ended the tile which last read that buffer)
-      constexpr bool kStw = kMore && x >= kHalf && (x - kHalf) % kSpread == 0 && (x - kHalf) / kSpread < kNcw;
+      // chunks [c0, c1) of this thread are written in this step
+      constexpr int c0 = x < kHalf ? 0 : ((x - kHalf) * kNcw + (X - kHalf) - 1) / (X - kHalf);
+      constexpr int c1 = x < kHalf ? 0 : ((x + 1 - kHalf) * kNcw + (X - kHalf) - 1) / (X - kHalf);
+      constexpr bool kStw = kMore && c1 > c0;
       constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
       if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
+      if constexpr (kRdKEarly) read_k(Kb, sb + 1, kf[0]);
       if constexpr (!kLean && kRdV) read_v(Vb, sb + 1, vf[(sb + 1) & 1]);
       if constexpr (x + 1 < X) qk(x + 1);
       ex(x);
-      if constexpr (kLeanK && kRdK) read_k(Kb, sb + 1, kf[0]);
+      if constexpr (kLeanK && kRdK && !kRdKEarly) read_k(Kb, sb + 1, kf[0]);
       if constexpr (x >= 1) pv(x - 1);
       if constexpr (kLean && kRdV) read_v(Vb, sb, vf[0]);
-      if constexpr (kStw) stage_write((x - kHalf) / kSpread, buf ^ 1, true, role);
+      if constexpr (kStw)
+#pragma unroll
+        for (int i = c0; i < c1; ++i) stage_write(i, buf ^ 1, kF16, role);
       if constexpr (SCHED) {
         // one MFMA per slot (this step's Q K^T first, then P V), the step's exponentials and
         // VALU spread evenly over the slots; LDS reads early, or (LEAN) after their last reader
@@ -393,8 +442,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
         constexpr int nq = x + 1 < X ? kNKT : 0;
         constexpr int nm = nq + (x >= 1 ? 2 * kNDT : 0);
         constexpr int ne = 16;
-        constexpr int nv = 8 + (kStwK ? 24 : 0) + (kMasked ? 32 : 0);
-        constexpr int nr = (!kLeanK && kRdK ? kNKT : 0) + (!kLean && kRdV ? 8 : 0);
+        constexpr int nv = 8 + (kF16 ? 0 : 16) + (kStwK && kF16 ? 24 * (c1 - c0) : 0) + (kMasked ? 32 : 0);
+        constexpr int nr = (!kLeanK && kRdK ? kNKT : 0) + (!kLean && kRdV ? 4 * kNDT : 0);
+        if constexpr (kRdKEarly) __builtin_amdgcn_sched_group_barrier(0x100, kNKT, 0);
         static_for<nm>([&](auto ic) __attribute__((always_inline)) {
           constexpr int i = decltype(ic)::value;
           constexpr int te = (ne * (i + 1)) / nm - (ne * i) / nm;
@@ -408,10 +458,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
             __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
           }
           if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, (nr * (i + 1)) / nm - (nr * i) / nm, 0);
-          if constexpr (kLeanK && kRdK && i >= nq && i < nq + kNKT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if constexpr (kStw && i < 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          if constexpr (kLeanK && kRdK && !kRdKEarly && i >= nq && i < nq + kNKT)
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if constexpr (kStw && i < 2) __builtin_amdgcn_sched_group_barrier(0x200, c1 - c0, 0);
         });
-        if constexpr (kLean && kRdV) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        if constexpr (kLean && kRdV) __builtin_amdgcn_sched_group_barrier(0x100, 4 * kNDT, 0);   // ds_read_b64_tr x2 per fragment
         __builtin_amdgcn_sched_barrier(0);
       }
     });
@@ -419,15 +470,28 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
     stamp(2 + 2 * kt);
     // row sums (O^T row 40 = d tile 1, register 4 of the low lane half): a sum past 2^64 moves
     // the reference point up by 64 (rounded to f16) and rescales O by the exact factor
+    // The last P V of block QB-1 was issued just above; its row sum is read after explicit padding
+    // and before the first rescale branch.  Without it the wait states the compiler put on the
+    // branch fall-through proved short on gfx950 (d = 80: the copy read for the lane-half swap
+    // saw the pre-MFMA value on one half, so the halves disagreed about the rescale)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    float lsums[QB];
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
-      const float own = O[b][1][4];
-      const float lsum = own + other_half(own);
+      const float own = O[b][kLdt][kLr];
+      lsums[b] = own + other_half(own);
+    }
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      const float lsum = lsums[b];
       bad |= !(lsum < INFINITY);
-      if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
-        if (lsum > 0x1p64f) {
-          const float mnew = (float)(_Float16)(m_ref[b] + 64.f);
-          ovf |= !(fabsf(mnew) < 65504.f);
+      constexpr float kResc = (FORM & 2048) ? 0x1p100f : 0x1p64f;   // FORM bit 2048: probe threshold
+      if (__builtin_expect(__any(lsum > kResc), 0)) {
+        if (lsum > kResc) {
+          const float mnew = kF16 ? (float)(_Float16)(m_ref[b] + 64.f) : m_ref[b] + 64.f;
+          ovf |= !(fabsf(mnew) < (kF16 ? 65504.f : INFINITY));
           const float f = fast_exp2(m_ref[b] - mnew);
 #pragma unroll
           for (int dt = 0; dt < kNDT; ++dt)
@@ -463,7 +527,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) nf = __builtin_fmaf(O[b][dt][r], 0.f, nf);   // NaN iff some O is inf/NaN
     bad |= !(nf == 0.f);
-    const bool any_bad = __any(bad || ovf);
+    const bool any_bad = __any(bad || ovf) || (FORM & 1024) != 0;   // FORM bit 1024: always recompute
     if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
   }
   __syncthreads();
@@ -522,74 +586,112 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   }
 
   stamp(36);
-  // ---- epilogue: O / l, rows 0-39 of O^T (q on the lane)
+  // ---- epilogue: O / l.  O^T has the query on the lane, so a direct store would touch 64 rows
+  // (64 cache lines) per instruction; the wave writes its rows to LDS instead (the tile buffers
+  // are dead: every wave has passed the last tile's barrier) and stores them back as contiguous
+  // 16-byte chunks, consecutive lanes along a row
+  uint16_t* const orow = smem + wave * (32 * QB * kOS);
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
-    const float l = __shfl(O[b][1][4], lane & 31);
+    const float l = __shfl(O[b][kLdt][kLr], lane & 31);
     const float inv = 1.f / l;
-    const int p = pw + 32 * b + qi;
-    if (p < a.P) {
-      uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * kD + (int64_t)p * a.ldo;
 #pragma unroll
-      for (int dt = 0; dt < kNDT; ++dt)
+    for (int dt = 0; dt < kNDT; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int dd = dt * 32 + 8 * g + 4 * hh;
-          if (dd < kD)
-            store4(op + dd, O[b][dt][4 * g] * inv, O[b][dt][4 * g + 1] * inv, O[b][dt][4 * g + 2] * inv,
-                   O[b][dt][4 * g + 3] * inv);
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int dd = dt * 32 + 8 * g + 4 * hh;
+        if (dd < kD)
+          store4(orow + (32 * b + qi) * kOS + dd, O[b][dt][4 * g] * inv, O[b][dt][4 * g + 1] * inv,
+                 O[b][dt][4 * g + 2] * inv, O[b][dt][4 * g + 3] * inv);
+      }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    constexpr int kChunks = 32 * QB * kCPR;
+    uint16_t* const obase = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * kD;
+#pragma unroll
+    for (int c0 = 0; c0 < kChunks; c0 += 64) {
+      const int cidx = c0 + lane;
+      const int row = cidx / kCPR, ch = cidx - (cidx / kCPR) * kCPR;
+      const int p = pw + row;
+      if ((kChunks % 64 == 0 || cidx < kChunks) && p < a.P)
+        *reinterpret_cast<short8_t*>(obase + (int64_t)p * a.ldo + ch * 8) =
+            *reinterpret_cast<const short8_t*>(orow + row * kOS + ch * 8);
     }
   }
   stamp(37);
 }
 
-template <int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
+template <int D, int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
 hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
-  hipLaunchKernelGGL((self40_kernel<WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
 }  // namespace
 
-bool self40_eligible(const SelfArgs& a) { return a.P >= 2048 && a.K >= 256; }
+bool self40_eligible(const SelfArgs& a, int d) {
+  if (d == 40) return a.P >= 2048 && a.K >= 256;
+  if (d == 80) return a.P >= 512 && a.K >= 256;
+  return false;
+}
 
-// variant: 0 = production shape; the experiments build also honours 62 (128-key tiles) and 64
-// (no scheduling directives)
-int run_self40(const SelfArgs& a, hipStream_t st) {
+// variant: 0 = production shapes; the experiments build also honours the A/B shapes below
+int run_self40(const SelfArgs& a, int d, hipStream_t st) {
 #ifdef S40_ONLY
   return (int)launch<S40_ONLY>(a, st);
 #else
+  if (d == 80) {
+    switch (a.variant) {
+#ifdef P2P_EXPERIMENTS
+      case 91: return (int)launch<80, 8, 2, 128, true, 1>(a, st);
+      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
+      case 93: return (int)launch<80, 4, 2, 128, true, 1 | 1024>(a, st);   // exact recompute only
+      case 94: return (int)launch<80, 4, 2, 128, true, 1 | 2048>(a, st);
+      case 95: return (int)launch<80, 4, 2, 128, false, 1>(a, st);
+      case 96: return (int)launch<80, 4, 2, 128, true, 0>(a, st);
+      case 97: return (int)launch<80, 4, 1, 128, true, 1 | 4096>(a, st);
+      case 98: return (int)launch<80, 4, 1, 64, true, 1 | 4096>(a, st);
+      case 99: return (int)launch<80, 4, 2, 64, true, 1>(a, st);
+      case 100: return (int)launch<80, 2, 2, 64, true, 1 | 4096>(a, st);
+      case 101: return (int)launch<80, 8, 1, 64, true, 1>(a, st);
+      case 102: return (int)launch<80, 8, 1, 128, true, 1>(a, st);
+      case 103: return (int)launch<80, 4, 2, 128, true, 1 | 16>(a, st);   // 92 with clock stamps
+#endif
+      default: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
+    }
+  }
   switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
-    case 62: return (int)launch<4, 2, 128>(a, st);
-    case 64: return (int)launch<4, 2, 256, false>(a, st);
-    case 61: return (int)launch<4, 2, 256>(a, st);
-    case 67: return (int)launch<8, 2, 256, true, 3>(a, st);
-    case 68: return (int)launch<4, 2, 256, true, 2>(a, st);
-    case 69: return (int)launch<4, 2, 256, true, 1>(a, st);
-    case 70: return (int)launch<8, 2, 128, true, 1>(a, st);
-    case 71: return (int)launch<8, 2, 256, true, 1 | 16>(a, st);   // the default shape with clock stamps
-    case 72: return (int)launch<8, 2, 256, true, 1 | 8>(a, st);
-    case 73: return (int)launch<8, 2, 256, true, 1 | 4>(a, st);
-    case 74: return (int)launch<8, 2, 256, true, 1 | 32>(a, st);        // priority flip at X/2
-    case 75: return (int)launch<8, 2, 256, true, 1 | 64>(a, st);        // at X/4
-    case 76: return (int)launch<8, 2, 256, true, 1 | 96>(a, st);        // at 3X/4
-    case 77: return (int)launch<8, 2, 256, true, 1 | 32 | 16>(a, st);   // 74 with clock stamps
-    case 78: return (int)launch<8, 2, 256, true, 1 | 128>(a, st);       // split staging
-    case 79: return (int)launch<8, 2, 256, true, 1 | 128 | 32>(a, st);  // split staging + flip at X/2
-    case 80: return (int)launch<8, 2, 256, true, 1 | 128 | 16>(a, st);  // 78 with clock stamps
-    case 81: return (int)launch<8, 2, 256, true, 1 | 128 | 256>(a, st);        // split + alternate every 2 steps
-    case 82: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // split + alternate every 4 steps
-    case 83: return (int)launch<8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // 81 with clock stamps
+    case 62: return (int)launch<40, 4, 2, 128>(a, st);
+    case 64: return (int)launch<40, 4, 2, 256, false>(a, st);
+    case 61: return (int)launch<40, 4, 2, 256>(a, st);
+    case 66: return (int)launch<40, 8, 2, 256, true, 1>(a, st);   // round-3 first LEAN default
+    case 67: return (int)launch<40, 8, 2, 256, true, 3>(a, st);
+    case 68: return (int)launch<40, 4, 2, 256, true, 2>(a, st);
+    case 69: return (int)launch<40, 4, 2, 256, true, 1>(a, st);
+    case 70: return (int)launch<40, 8, 2, 128, true, 1>(a, st);
+    case 71: return (int)launch<40, 8, 2, 256, true, 1 | 16>(a, st);   // 66 with clock stamps
+    case 72: return (int)launch<40, 8, 2, 256, true, 1 | 8>(a, st);
+    case 73: return (int)launch<40, 8, 2, 256, true, 1 | 4>(a, st);
+    case 74: return (int)launch<40, 8, 2, 256, true, 1 | 32>(a, st);        // priority flip at X/2
+    case 75: return (int)launch<40, 8, 2, 256, true, 1 | 64>(a, st);        // at X/4
+    case 76: return (int)launch<40, 8, 2, 256, true, 1 | 96>(a, st);        // at 3X/4
+    case 77: return (int)launch<40, 8, 2, 256, true, 1 | 32 | 16>(a, st);   // 74 with clock stamps
+    case 78: return (int)launch<40, 8, 2, 256, true, 1 | 128>(a, st);       // split staging
+    case 79: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 32>(a, st);  // split staging + flip at X/2
+    case 80: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 16>(a, st);  // 78 with clock stamps
+    case 82: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // alternate every 4 steps
+    case 83: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // default with clock stamps
 #endif
-    case 66: return (int)launch<8, 2, 256, true, 1>(a, st);   // round-3 first LEAN default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // alternate step pairs: G1 0.1931-0.1938 ms vs 0.1964 (66) and 0.2056 (round 2), profiles/r03
-    default: return (int)launch<8, 2, 256, true, 1 | 128 | 256>(a, st);
+    default: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);
   }
 #endif
 }

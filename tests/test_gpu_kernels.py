@@ -146,6 +146,26 @@ def test_self_attention_f16_form(cuda, case):
     assert (o.float() - want).abs().max().item() < bound
 
 
+@pytest.mark.parametrize("case", ["plain", "peaky32", "late_peak", "remap", "ragged", "g2"])
+def test_self_attention_d80_pipelined(cuda, case):
+    """The d = 80 production form (bf16 inputs, P >= 512, K >= 256; p2p_self40.hip, bf16 Q K^T
+    with p = exp2(fma(s, c, -m)), m from the first 32 keys): within the bf16 O bound on peaky rows;
+    a logit far above m in a later tile (late_peak) takes the exact recompute.  g2: the config-2
+    G2/G6 launch (N = 8, H = 8, P = K = 1024)."""
+    N, P, K, H, d = {"ragged": (2, 1100, 1100, 2, 80), "g2": (8, 1024, 1024, 8, 80)}.get(case, (2, 1024, 1024, 2, 80))
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=33)
+    if case == "late_peak":
+        q[0, 7, :d] = 60.0              # entry 0, head 0, query 7
+        k[0, 700, :d] = 60.0            # key 700 (tile 5 of 128): c s ~ 3.3e4 log2 units
+    src = [0, 0] if case == "remap" else None
+    o = torch.empty_like(q)
+    _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16", qk_src=src)
+    want = ref_out(ref_probs(q, k, H, d ** -0.5, qk_src=src), v, H)
+    assert torch.isfinite(o.float()).all()
+    bound = o_tol(v, "bf16") + 2.0 ** -8 * want.abs().max().item()
+    assert (o.float() - want).abs().max().item() < bound
+
+
 @pytest.mark.parametrize("io", [torch.bfloat16])
 def test_self_attention_bf16_io(cuda, io):
     N, P, K, H, d = 2, 1024, 1024, 8, 80

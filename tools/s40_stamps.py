@@ -2,7 +2,9 @@
 71 = the production shape with s_memtime stamps): prologue, per-tile compute, barrier wait per
 tile, recompute check + epilogue.  Stamps come from the first 256 workgroups of a config-2 G1
 launch (N = 8, H = 8, P = K = 4096, d = 40).
-Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=71 python tools/s40_stamps.py"""
+Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=71 python tools/s40_stamps.py
+       S40_STAMPS=P,d,waves,bk,qb (default 4096,40,8,256,2; the d = 80 stamped variant 103:
+       S40_STAMPS=1024,80,4,128,2)"""
 import ctypes
 import os
 import statistics
@@ -15,15 +17,18 @@ import torch  # noqa: E402
 
 from p2p_amd import _hip  # noqa: E402
 
-SLOTS, WAVES, NWG, NTILES = 40, 8, 256, 16
+SLOTS, NWG = 40, 256
+P, D, WAVES, BK, QB = (int(x) for x in os.environ.get("S40_STAMPS", "4096,40,8,256,2").split(","))
+NTILES = P // BK
+X = (BK // 32) * QB   # 32x32 blocks per tile per wave
 
 
 def main():
-    N, H, P, d = 8, 8, 4096, 40
+    N, H, P_, d = 8, 8, P, D
     C = H * d
-    q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
-    k = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
-    v = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
+    q = torch.randn(N, P_, C, device="cuda").to(torch.bfloat16)
+    k = torch.randn(N, P_, C, device="cuda").to(torch.bfloat16)
+    v = torch.randn(N, P_, C, device="cuda").to(torch.bfloat16)
     o = torch.empty_like(q)
     for _ in range(20):
         _hip.self_attn(q, k, v, o, H, d ** -0.5)
@@ -51,15 +56,15 @@ def main():
     print(f"cycles per wave (median over {NWG} workgroups x {WAVES} waves):")
     print(f"  total {med(tot):.0f}  prologue {med(pro):.0f}  compute/tile {med(comp):.0f} (x{NTILES} = {med(comp.sum(-1)):.0f})"
           f"  barrier/tile {med(bar):.0f} (x{NTILES} = {med(bar.sum(-1)):.0f})  check {med(chk):.0f}  epilogue {med(epi):.0f}")
-    print(f"  compute per 32x32 block: {med(comp) / 16:.0f} cycles per wave (2 waves per SIMD)")
+    print(f"  compute per 32x32 block: {med(comp) / X:.0f} cycles per wave")
     print(f"  tile 0 compute {med(comp[..., 0]):.0f}, tiles 1-{NTILES - 1} {med(comp[..., 1:]):.0f}")
     # younger half vs older half
-    print(f"  waves 0-3 compute/tile {med(comp[:, :4]):.0f} barrier/tile {med(bar[:, :4]):.0f};"
-          f" waves 4-7 compute/tile {med(comp[:, 4:]):.0f} barrier/tile {med(bar[:, 4:]):.0f}")
+    print(f"  older half compute/tile {med(comp[:, :WAVES // 2]):.0f} barrier/tile {med(bar[:, :WAVES // 2]):.0f};"
+          f" younger half compute/tile {med(comp[:, WAVES // 2:]):.0f} barrier/tile {med(bar[:, WAVES // 2:]):.0f}")
     # skew of barrier arrival within a workgroup
     arr = st[:, :, 2:2 + 2 * NTILES:2]
     skew = arr.max(1) - arr.min(1)
-    print(f"  arrival skew per tile (max-min over the 8 waves): median {med(skew):.0f}, p90 {float(np.percentile(skew, 90)):.0f}")
+    print(f"  arrival skew per tile (max-min over the waves): median {med(skew):.0f}, p90 {float(np.percentile(skew, 90)):.0f}")
     start_skew = t0.max(1) - t0.min(1)
     print(f"  workgroup start skew {med(start_skew):.0f}; workgroups' start spread {float(t0[:, 0].max() - t0[:, 0].min()):.0f}")
 
