@@ -774,12 +774,11 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
       for (int kt = 0; kt < nfull; ++kt) tile(kt, kNo, kNo, ex);
       if (nfull < ntiles) tile(nfull, kYes, kNo, ex);
     };
-    if constexpr (F16) {
-      if (wg_bad & 2) redo(kYes);
-      else redo(kNo);
-    } else {
-      redo(kNo);
-    }
+    // F16: every recompute (a range miss or a non-finite row sum) takes the exact bf16 path; a
+    // row-sum recompute on the F16 slow path could meet |m| >= 65504 on a later tile with nothing
+    // left to catch it
+    if constexpr (F16) redo(kYes);
+    else redo(kNo);
   }
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
