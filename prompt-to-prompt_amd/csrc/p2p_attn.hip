@@ -1562,23 +1562,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int count = rows * K;
       if (((uintptr_t)g & 15) == 0 && (count & 3) == 0) {
-        // all reads of the running sum first, then all writes: one memory round trip
-        constexpr int IT = (32 * KR / 4 + 63) / 64;
-        const int n4 = count / 4;
-        f32x4_t buf[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-          const int i = lane + 64 * j;
-          if (i < n4) {
-            buf[j] = reinterpret_cast<const f32x4_t*>(slab)[i];
-            if (a.store_accumulate) buf[j] += reinterpret_cast<const f32x4_t*>(g)[i];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-          const int i = lane + 64 * j;
-          if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
-        }
+        store_rows_rmw<32 * KR / 4>(g, slab, count, a.store_accumulate != 0, lane);
         // keeps the prefetch touches alive (never true: a running sum of probabilities is finite)
         if (__builtin_expect(touch0 == -INFINITY || touch1 == -INFINITY, 0)) g[0] = touch0 + touch1;
       } else {
@@ -1692,6 +1676,12 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && self40_eligible(a, 80) &&
         (a.variant == 0 || a.variant >= 91))
       return (hipError_t)run_self40(a, 80, st);
+  }
+  if constexpr (MP::kElemBytes == 2 && D == 160 && MQ::planes == 1 && sizeof(IO) == 2) {
+    // d = 160, bf16 inputs, O only (the 16x16 / 8x8 layers without kept maps or autograd): the
+    // waves of a 32-query workgroup split the keys (p2p_selfsplit.hip); variant 121 (experiments
+    // build) keeps the per-tile kernel below for A/B timing
+    if (mode == MODE_FUSED && self_split_eligible(a, D) && a.variant != 121) return (hipError_t)run_self_split(a, D, st);
   }
   if (mode == MODE_FUSED) {
     // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)
@@ -1876,6 +1866,7 @@ int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t 
     return dispatch_cross<float, QkF32, MmaF32>(a, d, st);
   }
   if (io_dtype == P2P_DTYPE_F32) return dispatch_cross<float, QkSplit, MmaBf16>(a, d, st);
+  if (cross_group_eligible(a, d)) return run_cross_group(a, d, st);
   return dispatch_cross<uint16_t, QkBf16<uint16_t>, MmaBf16>(a, d, st);
 }
 

@@ -157,6 +157,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     covered += G.count;
   }
   if (covered != t->n_batch) return P2P_E_BATCH;
+  a.n_groups = n_groups;
   bool any_store = false;
   for (int n = 0; n < t->n_batch; ++n) {
     a.store_slot[n] = (store && store_slot) ? store_slot[n] : -1;

@@ -40,6 +40,7 @@ struct CrossArgs {
   int N, P, K, H;
   float scale_log2;
   int n_qtiles;
+  int n_groups;                  // prompt groups (grp_* entries)
   float* store;
   int store_accumulate;
   int any_store;                 // some entry stores its maps
@@ -75,10 +76,16 @@ int run_self_maps(const SelfArgs& a, int io_dtype, int compute, int d, hipStream
 // materialise protocol: probs (a.store) [N*H, P, K] = softmax(Q K^T * scale), optional key mask
 int run_self_probs(const SelfArgs& a, int io_dtype, int compute, int d, hipStream_t st);
 int run_cross(const CrossArgs& a, int io_dtype, int compute, int d, hipStream_t st);
+// group-coupled cross-attention (p2p_cross.hip): bf16 inputs and compute, dense or no programs
+bool cross_group_eligible(const CrossArgs& a, int d);
+int run_cross_group(const CrossArgs& a, int d, hipStream_t st);
 // d = 40 / 80 self-attention with bf16 inputs, O only (p2p_self40.hip): the G1/G7 and G2/G6
 // production kernels
 bool self40_eligible(const SelfArgs& a, int d);
 int run_self40(const SelfArgs& a, int d, hipStream_t st);
+// d = 160 self-attention with bf16 inputs, O only, K <= 256 (p2p_selfsplit.hip): key-split waves
+bool self_split_eligible(const SelfArgs& a, int d);
+int run_self_split(const SelfArgs& a, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);
 

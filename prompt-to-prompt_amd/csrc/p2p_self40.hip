@@ -688,6 +688,12 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 80: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 16>(a, st);  // 78 with clock stamps
     case 82: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // alternate every 4 steps
     case 83: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // default with clock stamps
+    // two 4-wave workgroups per CU (128-key tiles, 78 KB of LDS each): the SIMD's second wave
+    // belongs to another workgroup, so one workgroup's barrier wait overlaps the other's compute
+    case 104: return (int)launch<40, 4, 2, 128, true, 1 | 4096>(a, st);
+    case 105: return (int)launch<40, 4, 2, 128, true, 1 | 128 | 4096>(a, st);
+    case 106: return (int)launch<40, 4, 2, 64, true, 1 | 4096>(a, st);
+    case 107: return (int)launch<40, 4, 2, 128, true, 1 | 16 | 4096>(a, st);   // 104 with clock stamps
 #endif
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // alternate step pairs: G1 0.1931-0.1938 ms vs 0.1964 (66) and 0.2056 (round 2), profiles/r03

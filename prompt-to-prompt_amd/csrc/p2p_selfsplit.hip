@@ -1,0 +1,210 @@
+// Key-split self-attention for the small SD geometries (16x16 and 8x8 layers: P = K <= 256 at
+// d = 160, ptp_utils.py:195-206), bf16 inputs, O only (no kept maps, no autograd).
+//
+// At these sizes a (entry, head) is 256 x 256 x 160: the per-tile kernel walks 8 key tiles one
+// global round trip after another, on 128 workgroups.  Here one workgroup = one 32-query block
+// of one (entry, head), and its W waves split the KEYS: wave w owns keys [w KW, (w+1) KW).
+// Every wave issues all of its loads at once -- its V rows go global -> LDS by DMA
+// (global_load_lds, no VGPRs), its K rows straight into A-operand registers (key on the lane),
+// Q into B-operand registers -- so the whole workgroup waits ONE round trip.  Then
+//   S^T = K_w Q^T (MFMA), m_w = row max over the wave's keys, p = exp2(c s - m_w),
+//   l_w = sum p (f32), O_w^T = V_w^T P^T (bf16 MFMA, V^T fragments by ds_read_b64_tr_b16),
+// each wave writes (O_w, m_w, l_w) into its own (now dead) V region, one barrier, and the
+// workgroup combines:  O = sum_w O_w 2^(m_w - M) / sum_w l_w 2^(m_w - M),  M = max_w m_w.
+// qk_src implements the source-map injection (Q, K of entry qk_src[n], V of n).
+#include "p2p_device.h"
+#include "p2p_kernels.h"
+
+namespace p2p {
+namespace {
+
+// D: head dim (multiple of 32, no padding columns); W waves x KBW 32-key blocks per wave
+template <int D, int W, int KBW>
+__global__ __launch_bounds__(64 * W, 2) void self_split_kernel(SelfArgs a) {
+  static_assert(D % 32 == 0, "d tiles without padding");
+  constexpr int NKT = D / 16;      // 16-deep k steps of Q K^T
+  constexpr int NDT = D / 32;      // 32-row tiles of O^T
+  constexpr int KW = 32 * KBW;     // keys per wave
+  constexpr int VROW = D * 2;      // bytes per V row in LDS (dense: one DMA instruction = 1 KiB)
+  static_assert(VStrideBf16<D>::value == D, "dense V rows are conflict-free for the transposed reads");
+  constexpr int VREG = KW * VROW;  // bytes of one wave's V region
+  constexpr int OS = D + 4;          // O partial row stride (floats): rows on distinct banks
+  constexpr int OREG = 32 * OS * 4;  // its O partial: [32 rows][OS] f32
+  constexpr int REG = VREG > OREG ? VREG : OREG;
+  __shared__ __attribute__((aligned(16))) char smem[W * REG];
+  __shared__ float ml[W][2][32];      // m_w, l_w of every row
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qi = lane & 31;
+
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H;
+  const int n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int K = a.K;
+  const float c = a.scale_log2;
+  const int p = qt * 32 + qi;
+  const bool prow = p < a.P;
+  const int key0 = wave * KW;
+
+  const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * D;
+  char* const reg = smem + wave * REG;
+  uint16_t* const Vw = reinterpret_cast<uint16_t*>(reg);
+
+  // ---- every load of this wave at once.  V: row r of the wave (key key0 + r) lands at
+  // Vw + r * D; one DMA instruction moves 64 x 16 bytes = 1024 / VROW rows.  Rows past K read
+  // row K-1 (their p is 0; any finite value will do).
+  {
+    constexpr int CPR = D / 8;                 // 16-byte chunks per row
+    constexpr int NI = KW * CPR / 64;          // DMA instructions per wave
+    static_assert((KW * CPR) % 64 == 0, "whole instructions");
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int cidx = i * 64 + lane;
+      const int r = cidx / CPR;
+      const int ch = cidx - r * CPR;
+      const int key = min(key0 + r, K - 1);
+      const uint16_t* g = vp + (int64_t)key * a.ldv + ch * 8;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
+                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                           reinterpret_cast<uintptr_t>(Vw + i * 512)),
+                                       16, 0, 0);
+    }
+  }
+  short8_t qf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+    qf[t] = prow ? *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + 16 * t + 8 * hh) : short8_t{};
+  short8_t kf[KBW][NKT];
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb) {
+    const int key = min(key0 + kb * 32 + qi, K - 1);
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) kf[kb][t] = *reinterpret_cast<const short8_t*>(kp + (int64_t)key * a.ldk + 16 * t + 8 * hh);
+  }
+
+  // ---- S^T = K_w Q^T, the wave's row max and exponentials
+  float sv[KBW][16];
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb) {
+    f32x16_t acc = {};
+#pragma unroll
+    for (int t = 0; t < NKT; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf[kb][t]),
+                                                    __builtin_bit_cast(bf16x8_t, qf[t]), acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      sv[kb][r] = (key0 + kb * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[kb][r]);
+  mx = fmaxf(mx, other_half(mx)) * c;   // every wave owns >= 1 key below K: mx is finite
+  float ls = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = fast_exp2(fmaf(sv[kb][r], c, -mx));
+      sv[kb][r] = e;
+      ls += e;
+    }
+  ls += other_half(ls);
+
+  // ---- O_w^T = V_w^T P^T once the wave's V rows have landed
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA (and every other load) retired
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  f32x16_t O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb) pv_block<D, NDT>(MmaBf16{}, O, Vw, kb * 32, sv[kb], lane);
+
+  // ---- the partial into the wave's own region (its V is dead once every lane's reads are in):
+  // O_w as [32 rows][OS] f32; m_w, l_w per row beside it
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float* const Ow = reinterpret_cast<float*>(reg);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4_t*>(Ow + qi * OS + dt * 32 + 8 * g + 4 * hh) =
+          f32x4_t{O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2], O[dt][4 * g + 3]};
+  if (hh == 0) {
+    ml[wave][0][qi] = mx;
+    ml[wave][1][qi] = ls;
+  }
+  __syncthreads();
+
+  // ---- combine: thread t -> (row, 4-column chunk) pairs, whole rows of O out as bf16
+  constexpr int CH = 32 * D / 4;   // 4-column chunks of the 32 x D block
+  for (int i = tid; i < CH; i += 64 * W) {
+    const int row = i / (D / 4);
+    const int col = (i - row * (D / 4)) * 4;
+    float m[W], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      m[w] = ml[w][0][row];
+      M = fmaxf(M, m[w]);
+    }
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const float* ow = reinterpret_cast<const float*>(smem + w * REG);
+      const float f = fast_exp2(m[w] - M);
+      L += ml[w][1][row] * f;
+      acc += *reinterpret_cast<const f32x4_t*>(ow + row * OS + col) * f;
+    }
+    const int pr = qt * 32 + row;
+    if (pr < a.P) {
+      const float inv = 1.f / L;
+      uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)pr * a.ldo + col;
+      store4(op, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    }
+  }
+}
+
+template <int D, int W, int KBW>
+hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 31) / 32;
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_split_kernel<D, W, KBW>), grid, block, 0, st, b);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// d = 160, bf16 inputs, O only, K <= 128 (the 8x8 layers): the waves split the keys (W =
+// ceil(K / 64) waves of 64 keys, or 2 x 32 for K <= 64).  Measured against the per-tile kernel
+// (tools/small_bench.py, profiles/r03/small): 8x8 (K = 64) 7.84 -> 6.21 us; 16x16 (K = 256)
+// 14.73 -> 16.51 us -- every 32-query workgroup then pulls the head's whole K and V through its
+// CU (4x the per-tile kernel's L2 -> CU traffic), so K > 128 keeps the per-tile kernel
+bool self_split_eligible(const SelfArgs& a, int d) {
+  return d == 160 && a.K >= 1 && a.K <= 128 && a.lse == nullptr && a.n_maps == 0;
+}
+
+int run_self_split(const SelfArgs& a, int d, hipStream_t st) {
+  (void)d;
+  if (a.K <= 32) return (int)launch_split<160, 1, 1>(a, st);
+  if (a.K <= 64) return (int)launch_split<160, 2, 1>(a, st);
+  if (a.K <= 128) return (int)launch_split<160, 2, 2>(a, st);
+  if (a.K <= 192) return (int)launch_split<160, 3, 2>(a, st);
+  return (int)launch_split<160, 4, 2>(a, st);
+}
+
+}  // namespace p2p

@@ -10,7 +10,7 @@ import os
 
 _CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 # every file whose text reaches the compiler or the link line, in a fixed order
-FILES = ("p2p_attn.hip", "p2p_self40.hip", "p2p_bwd.hip", "p2p_blend.hip", "p2p_capi.hip", "p2p_device.h", "p2p_kernels.h",
+FILES = ("p2p_attn.hip", "p2p_self40.hip", "p2p_selfsplit.hip", "p2p_cross.hip", "p2p_bwd.hip", "p2p_blend.hip", "p2p_capi.hip", "p2p_device.h", "p2p_kernels.h",
          "../../include/p2p_hip.h", "Makefile")
 
 

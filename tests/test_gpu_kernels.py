@@ -297,3 +297,86 @@ def test_store_scale(cuda):
     for steps in (7, 50, 3):
         y = _hip.store_scale(x, float(steps))
         assert torch.equal(y, x / steps)
+
+
+def _edit_mapper(B, K, weight=0.5):
+    m = torch.zeros(B - 1, K, K)
+    m[:, torch.arange(K), torch.arange(K)] = 1.0
+    m[0, 3, 3] = m[0, 4, 3] = weight
+    if B > 2:
+        m[1, 7, 7], m[1, 7, 8] = 0.0, 1.0
+        m[1, 8, 8], m[1, 8, 7] = 0.0, 1.0
+    return m
+
+
+@pytest.mark.parametrize("geom", [(4096, 40, 77), (1024, 80, 77), (256, 160, 77), (64, 160, 77), (100, 80, 96),
+                                  (333, 40, 33)], ids=lambda g: "x".join(map(str, g)))
+@pytest.mark.parametrize("n_groups", [1, 2])
+def test_cross_group_kernel_bf16(cuda, geom, n_groups):
+    """The group-coupled cross kernel (bf16 inputs: p2p_cross.hip): [uncond groups | cond groups],
+    each cond group a source + 3 dense Replace edits against its OWN source (main.py:185-193), the
+    cond maps kept and accumulated over two calls, LocalBlend word sums folded in, against fp32
+    einsum on the same bf16 inputs.  Covers G1-G4, ragged P, K = 96 (no short tail), K = 33."""
+    from p2p_amd import programs
+    P, d, K = geom
+    B, H = 4, 8
+    N = 2 * B * n_groups
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=6.0, seed=31 + P)
+    scale = d ** -0.5
+    mappers = [_edit_mapper(B, K), _edit_mapper(B, K).flip(0)][:n_groups]
+    progs = [programs.replace_program(m).to_device(cuda) for m in mappers]
+    alpha = torch.ones(B - 1, K, device=cuda)      # edit 0: alpha 1 everywhere (R only)
+    alpha[1] = 0.0                                   # edit 1: alpha 0 everywhere (own P only)
+    alpha[2, 10:20] = 0.0                            # edit 2: both halves
+    lh = 5 * H
+    bsums = [torch.zeros(B, 2, lh, P, device=cuda) for _ in range(n_groups)]
+    balpha = torch.rand(B, K, device=cuda, generator=torch.Generator(device=cuda).manual_seed(5))
+    bsub = torch.rand(B, K, device=cuda, generator=torch.Generator(device=cuda).manual_seed(6))
+    BG = B * n_groups
+    groups = [(g * B, B, None, None) for g in range(n_groups)]
+    groups += [(BG + g * B, B, progs[g], alpha, (bsums[g], balpha, bsub if g == 0 else None, 2 * H, lh))
+               for g in range(n_groups)]
+    store = torch.zeros(BG * H, P, K, device=cuda)
+    slots = [-1] * BG + [i * H for i in range(BG)]
+    o = torch.empty_like(q)
+    for acc in (False, True):
+        _hip.cross_attn(q, k, v, o, H, scale, groups, store=store, store_slot=slots, accumulate=acc)
+    p = ref_probs(q, k, H, scale)                                    # [N, H, P, K]
+    want = p.clone()
+    for g in range(n_groups):
+        s0 = BG + g * B
+        base = p[s0]
+        R = torch.einsum("hpw,bwn->bhpn", base, mappers[g].to(cuda))
+        a = alpha[:, None, None, :]
+        want[s0 + 1:s0 + B] = R * a + (1 - a) * p[s0 + 1:s0 + B]
+    cond = want[BG:]
+    assert (store - 2 * cond.reshape(BG * H, P, K)).abs().max().item() < 2 * 2e-3
+    assert (o.float() - ref_out(want, v, H)).abs().max().item() < o_tol(v, "bf16")
+    for g in range(n_groups):
+        c = cond[g * B:(g + 1) * B]                                  # [B, H, P, K]
+        ws_a = torch.einsum("bhpk,bk->bhp", c, balpha)
+        got = bsums[g][:, 0, 2 * H:3 * H]
+        assert (got - 2 * ws_a).abs().max().item() < 2e-2
+        got_s = bsums[g][:, 1, 2 * H:3 * H]
+        ws_s = torch.einsum("bhpk,bk->bhp", c, bsub) if g == 0 else torch.zeros_like(ws_a)
+        assert (got_s - 2 * ws_s).abs().max().item() < 2e-2
+        assert bsums[g][:, :, :2 * H].abs().max().item() == 0.0 and bsums[g][:, :, 3 * H:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("case", ["g3", "g4", "peaky32", "remap", "ragged", "k200", "k33", "k20"])
+def test_self_attention_key_split_d160(cuda, case):
+    """d = 160 with bf16 inputs, O only: K <= 128 takes the key-split kernel (p2p_selfsplit.hip: the
+    waves of a 32-query workgroup split the keys and combine (O_w, m_w, l_w) in LDS), larger K the
+    per-tile kernel.  g4 / g3: the config-2 8x8 and 16x16 launches; ragged P / K and key-split wave
+    counts 1 and 2 (K = 20, 33, 77); K = 200 and 256 on the per-tile path."""
+    N, P, K, H, d = {"g3": (8, 256, 256, 8, 160), "g4": (8, 64, 64, 8, 160), "ragged": (3, 100, 77, 2, 160),
+                     "k200": (2, 130, 200, 4, 160), "k33": (2, 70, 33, 2, 160),
+                     "k20": (2, 45, 20, 2, 160)}.get(case, (4, 256, 256, 4, 160))
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=41)
+    src = [0, 1, 0, 0] if case == "remap" else None
+    o = torch.empty_like(q)
+    _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16", qk_src=src)
+    want = ref_out(ref_probs(q, k, H, d ** -0.5, qk_src=src), v, H)
+    assert torch.isfinite(o.float()).all()
+    bound = o_tol(v, "bf16") + 2.0 ** -8 * want.abs().max().item()
+    assert (o.float() - want).abs().max().item() < bound
