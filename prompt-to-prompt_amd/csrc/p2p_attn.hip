@@ -563,8 +563,10 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
         bool staged = false;
         if constexpr (F16) if constexpr (!decltype(ex)::value) {
           staged = true;
-          // bf16 -> f16 is exact inside the f16 range (8 significant bits); RTZ packing, so a
-          // value past 65504 would clamp silently: range-checked instead
+          // bf16 -> f16 is exact for magnitudes in [2^-14, 65504] (8 significant bits); below
+          // 2^-14 f16 subnormals keep fewer bits (absolute error < 2^-25, flush to 0 under 2^-25),
+          // negligible beside the logits.  RTZ packing would clamp past 65504 silently: the range
+          // is checked instead
           short8_t hv;
           float mx = 0.f;
 #pragma unroll
@@ -725,14 +727,18 @@ __global__ __launch_bounds__(64 * WAVES) void self_attn_multi_kernel(SelfArgs a)
         bad |= !(lsum < INFINITY);
         if (__builtin_expect(__any(lsum > 0x1p64f), 0)) {
           if (lsum > 0x1p64f) {
+            // the new reference is rounded first (F16: it must be exact in Q's f16 column) and
+            // O rescaled by the exact factor between the two, so old and new tiles stay consistent
+            const float mnew = kF16 ? (float)(_Float16)(m_run[b] + 64.f) : m_run[b] + 64.f;
+            const float f = fast_exp2(m_run[b] - mnew);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) O[b][dt][r] *= 0x1p-64f;
-            m_run[b] += 64.f;
+              for (int r = 0; r < 16; ++r) O[b][dt][r] *= f;
+            m_run[b] = mnew;
             if constexpr (kF16) {
-              ovf |= !(fabsf(m_run[b]) < 65504.f);
-              set_mcol(b, m_run[b]);
+              ovf |= !(fabsf(mnew) < 65504.f);
+              set_mcol(b, mnew);
             }
           }
         }

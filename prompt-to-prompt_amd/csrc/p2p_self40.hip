@@ -239,8 +239,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
           vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)voff[i], 0, 0));
       }
   };
-  // chunk i into LDS buffer buf: K as f16 (fast form; exact inside the f16 range, RTZ packing
-  // would clamp past 65504 silently, so the range is checked) or raw bf16 (exact path)
+  // chunk i into LDS buffer buf: K as f16 (fast form; exact for magnitudes in [2^-14, 65504] --
+  // smaller ones become f16 subnormals, absolute error < 2^-25 --, RTZ packing would clamp past
+  // 65504 silently, so the range is checked) or raw bf16 (exact path)
   auto stage_write = [&](int i, int buf, bool as_f16, auto role) __attribute__((always_inline)) {
     constexpr int kRole = decltype(role)::value;
     if (!chunk_live(i, role)) return;

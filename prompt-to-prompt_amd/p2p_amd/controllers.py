@@ -375,12 +375,18 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
     # of the 12.6 MB of maps every step.  Valid only while EVERY step folded all five layers.
     BLEND_SLOTS = {("down_cross", 2): 0, ("down_cross", 3): 1, ("up_cross", 0): 2, ("up_cross", 1): 3,
                    ("up_cross", 2): 4}
+    # The fold sums each step's word sums (sum over steps of sum over words) where the reference
+    # takes the word sums of the summed maps (main.py:37-44): equal in exact arithmetic, a
+    # different f32 summation order in practice, so a pixel sitting on the threshold can flip
+    # (tests/test_gpu_blend_fold.py pins the agreement).  False = strict parity: the blend reads
+    # the stored maps as the reference does.
+    fold_local_blend = True
 
     def _blend_fold(self, key_idx, P, K, heads, device):
         """The p2p_group.blend_* tuple for this stored cross layer, or None."""
         lb = self.local_blend
         slot = self.BLEND_SLOTS.get(key_idx)
-        if slot is None or lb is None or P != 256 or not (_owned(lb, "__call__") and hasattr(lb, "_fold_tables")):
+        if not self.fold_local_blend or slot is None or lb is None or P != 256 or not (_owned(lb, "__call__") and hasattr(lb, "_fold_tables")):
             return None
         alpha, sub = lb._fold_tables()
         if alpha.shape != (self.batch_size, K) or alpha.device != device:

@@ -22,8 +22,7 @@ STEPS = 16   # LocalBlend starts after int(0.2 * 50) = 10 steps
 def _run(model, prompts, fold, masks):
     with config.compute_mode("bf16"):
         ctrl = pl.make_replace_controller(prompts, STEPS, device=model.device)
-        if not fold:
-            ctrl._blend_fold = lambda *a, **k: None
+        ctrl.fold_local_blend = fold      # False: the strict-parity map path
         lb = ctrl.local_blend
         orig = lb.step_mask
 

@@ -117,7 +117,7 @@ def test_bf16_inputs_exact_products(cuda):
 
 
 @pytest.mark.parametrize("case", ["plain", "peaky32", "k_past_f16", "q_past_f16", "late_peak", "remap", "ragged",
-                                  "g1"])
+                                  "g1", "multi_late_peak"])
 def test_self_attention_f16_form(cuda, case):
     """The d = 40 production form (bf16 inputs, P >= 2048; p2p_self40.hip): Q prescaled by
     scale*log2(e) in f16, K staged as f16, -m in Q's padding column, the reference point m taken
@@ -125,7 +125,8 @@ def test_self_attention_f16_form(cuda, case):
     (|k| >= 65520, |c q| >= 65520) and a logit far above m in a later tile (late_peak: c s ~ 5.7e5
     with q and k inside the f16 range) take the exact bf16 recompute and stay exact.  g1: the
     config-2 launch itself (N = 8, H = 8, P = K = 4096), held to o_tol + one bf16 output ulp."""
-    N, P, K, H, d = {"ragged": (2, 2100, 2100, 2, 40), "g1": (8, 4096, 4096, 8, 40)}.get(case, (2, 2048, 2048, 2, 40))
+    N, P, K, H, d = {"ragged": (2, 2100, 2100, 2, 40), "g1": (8, 4096, 4096, 8, 40),
+                     "multi_late_peak": (2, 2048, 200, 2, 40)}.get(case, (2, 2048, 2048, 2, 40))
     q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=31)
     if case == "k_past_f16":
         k[1, 100, 3] = 70000.0          # one key element of entry 1, head 0
@@ -136,6 +137,11 @@ def test_self_attention_f16_form(cuda, case):
     if case == "late_peak":
         q[0, 7, :d] = 250.0             # entry 0, head 0, query 7: c q ~ 57
         k[0, 1500, :d] = 250.0          # key 1500 (tile 5): c s ~ 5.7e5, tile 0 stays ordinary
+    if case == "multi_late_peak":
+        # K < 256: the F16 multi-block kernel (128-key tiles); tile 0 ordinary, key 150 (tile 1)
+        # with in-range q and k but c s ~ 5.7e5 > 65504: the recompute must take the exact path
+        q[0, 7, :d] = 250.0
+        k[0, 150, :d] = 250.0
     src = [0, 0] if case == "remap" else None
     o = torch.empty_like(q)
     _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16", qk_src=src)
