@@ -1048,11 +1048,11 @@ __global__ __launch_bounds__(256) void self_probs_kernel(SelfArgs a, int kw) {
 // plain launch runs at the occupancy of its K/V tiles alone.
 #ifdef P2P_EXPERIMENTS
 // diagnostic clock stamps of the cross kernel (experiments build, P2P_SELF_VARIANT 90):
-// [logical workgroup < 4096][wave < 4][slot < 16]; read back by p2p_diag_cross_stamps
-__device__ unsigned long long g_cross_stamps[4096 * 4 * 16];
+// [logical workgroup < 4096][wave < 4][slot < 24]; read back by p2p_diag_cross_stamps
+__device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #define P2P_CROSS_STAMP(i)                                                                              \
   if (a.variant == 90 && logical < 4096 && wave < 4 && lane == 0)                                       \
-    g_cross_stamps[(logical * 4 + wave) * 16 + (i)] = __builtin_amdgcn_s_memtime();
+    g_cross_stamps[(logical * 4 + wave) * 24 + (i)] = __builtin_amdgcn_s_memtime();
 #else
 #define P2P_CROSS_STAMP(i)
 #endif
@@ -1380,8 +1380,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   // dense edit (bf16 PV path, program carries the f16 mapper tile): R = P0 . M_e on the MFMA
   constexpr bool kDenseOk = DENSE && MP::kElemBytes == 2;  // separate instantiation: its VGPRs
   constexpr int kDenseTile = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * 2;  // bytes of the f16 tile
+  // the dense edit's per-column blend coefficients A | B: static LDS, so the store epilogue's
+  // per-wave slab (which overlays the dead mapper tile) never overlaps them
+  __shared__ __attribute__((aligned(16))) float dcol[kDenseOk ? 2 * KR : 4];
   const bool dense = kDenseOk && edit;   // the launcher picks DENSE only if every edit group is
   f32x16_t Rd[KB];
+  int dense_flags = 3;   // dense edits: the blend halves in use (set from the coefficients)
   if constexpr (kDenseOk) {
    if (dense) {
     const uint16_t* mg = static_cast<const uint16_t*>(a.grp_dense[gi]) +
@@ -1418,7 +1422,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     }
     {  // per-column coefficients next to the tile, read back after the barriers:
       // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B
-      float* col = reinterpret_cast<float*>(cross_dyn + kDenseTile);
+      float* col = dcol;
       if (w < KR) {
         const float ap = aw * pw;
         col[w] = fmaf(ap, cw, 1.f - aw);
@@ -1428,12 +1432,23 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     store_kv(kc0, vc0, false);
     __syncthreads();
     P2P_CROSS_STAMP(8)
+    {
+      // which blend halves the row uses (every wave scans the coefficients itself): bit 0 some
+      // A != 0 -> this edit's own softmax, bit 1 some B != 0 -> P0 and R.  A Replace step with
+      // alpha = 1 on every word (main.py:189) needs only R, one with alpha = 0 only its own P_b;
+      // dropping the other half is exact (fma(P, 0, x) = x, fma(P, A, R * 0) = P A)
+      const float* col = dcol;
+      const int c0 = lane, c1 = lane + 64;
+      const bool a0 = c0 < K && col[c0] != 0.f, a1 = c1 < K && col[c1] != 0.f;
+      const bool b0 = c0 < K && col[KR + c0] != 0.f, b1 = c1 < K && col[KR + c1] != 0.f;
+      dense_flags = (__any(a0 || a1) ? 1 : 0) | (__any(b0 || b1) ? 2 : 0);
+    }
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) Rd[kb] = f32x16_t{};
+    if (dense_flags & 2) {
     float p0[KB][16];
     probs(qf, p0);
     P2P_CROSS_STAMP(9)
-    load_q(n, qf);
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) Rd[kb] = f32x16_t{};
     // R = M^T P0 on the f16 MFMA: the mapper weights (1, 1/2, 1/4, ...) are exact in f16 and P0 in
     // [0, 1] rounds to 11 significant bits (|dR| <= 2^-12 R, inside the 2e-3 bar); every mapper
     // fragment read once; one 32-key block at a time (the scheduler would otherwise hoist all 18
@@ -1455,6 +1470,8 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
         }
       }
     }
+    }
+    load_q(n, qf);
     __syncthreads();  // every wave is done with the source K tile and the mapper tile
     P2P_CROSS_STAMP(10)
    }
@@ -1480,13 +1497,20 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   stage(n, true);
   __syncthreads();
   P2P_CROSS_STAMP(11)
-  probs(qf, sv);
+  if (!dense || (dense_flags & 1)) {
+    probs(qf, sv);
+  } else {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[kb][r] = 0.f;   // A = 0 on every column: P' = R B
+  }
   P2P_CROSS_STAMP(12)
 
   if (dense) {
     // a lane's columns come in runs of 4 (r & 3): one 16-byte LDS read per run and table;
     // one 32-column block at a time (hoisting every read costs ~150 VGPRs)
-    const float* const col = reinterpret_cast<const float*>(cross_dyn + kDenseTile);
+    const float* const col = dcol;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
@@ -1542,7 +1566,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   P2P_CROSS_STAMP(13)
   // ---- AttentionStore epilogue: post-edit maps, whole rows through the wave's slab
   if (stored) {
-    __syncthreads();  // every lane of the wave is done gathering from the slab
+    // the slab is this wave's own region: wave-level ordering suffices (the dense tile under it
+    // died at the post-R barrier; the term-plane path's P0 gather reads only this wave's slab)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
@@ -1550,7 +1578,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
         const int w = kb * 32 + acc_row(r, hh);
         if (w < K) slab[qi * K + w] = sv[kb][r];
       }
-    __syncthreads();
+    P2P_CROSS_STAMP(16)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    P2P_CROSS_STAMP(17)
     const int rows = min(32, a.P - p0w);
     // LocalBlend's word sums of these rows (lanes 0-31: alpha, 32-63: substruct), folded here so
     // the blend never re-reads the maps; words summed in index order as blend_wordsum_kernel does
@@ -1559,11 +1591,13 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
       if ((hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi]) != nullptr) {
         const float* tab = btab[hh];
         const float* row = slab + qi * K;
-        for (int w = 0; w < K; ++w) acc += row[w] * tab[w];
+#pragma unroll 8
+        for (int w = 0; w < K; ++w) acc += row[w] * tab[w];   // one sequential chain: the reads run ahead
       }
       float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w + qi;
       *dst = a.store_accumulate ? *dst + acc : acc;
     }
+    P2P_CROSS_STAMP(18)
     if (rows > 0) {
       float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int count = rows * K;
@@ -1707,6 +1741,11 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
         return hipGetLastError();
       }
     }
+#ifdef P2P_EXPERIMENTS
+    // 124: 64-key tiles at d >= 128 (half the per-tile round trips; 84 KB of LDS)
+    if constexpr (D >= 128 && MP::kElemBytes == 2)
+      if (a.variant == 124 && a.P > 64) { launch_fused<IO, MQ, MP, D, 64, 4>(a, st); return hipGetLastError(); }
+#endif
     if (a.P <= 64) launch_fused<IO, MQ, MP, D, BK, 2>(a, st);
     else launch_fused<IO, MQ, MP, D, BK, 4>(a, st);
     return hipGetLastError();
@@ -1733,8 +1772,7 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   const bool dense = kDense && a.edit_dense && !a.edit_terms;
   b.slab = (a.any_store || ((a.edit_terms || a.edit_dense) && !dense)) ? 1 : 0;
   size_t dyn = b.slab ? (size_t)W * 32 * b.slab_stride * sizeof(float) : 0;
-  const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t) +
-                      2 * P2P_MAX_KEYS_CROSS * sizeof(float);
+  const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
   if (dense)

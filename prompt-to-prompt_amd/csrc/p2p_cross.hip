@@ -378,7 +378,8 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, EDIT, STORE>())) void c
           if ((hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi]) != nullptr) {
             const float* tab = btab + hh * KR;
             const float* row = slab + qi * K;
-            for (int w = 0; w < K; ++w) acc += row[w] * tab[w];
+#pragma unroll 8
+            for (int w = 0; w < K; ++w) acc += row[w] * tab[w];   // one sequential chain: the reads run ahead
           }
           float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * P + p0w + qi;
           *dst = a.store_accumulate ? *dst + acc : acc;

@@ -288,29 +288,32 @@ __device__ __forceinline__ void store4(uint16_t* dst, float a, float b, float c,
 
 // AttentionStore read-add-write of one wave's [rows][K] block of post-edit maps: g (16-byte
 // aligned, cnt = rows * K floats, cnt % 4 == 0) (+)= slab (the wave's LDS copy of the rows).
-// The running-sum reads are range-checked buffer loads (zeros past cnt) issued unconditionally
-// in batches of MAXF4 / 64 / 2, so each batch costs ONE memory round trip (a read inside an
-// `if (i < n)` makes the compiler wait for it before the next one); only the stores are masked.
+// Every running-sum read is issued first -- range-checked buffer loads (zeros past cnt), no
+// branch, so they all fly together -- and only then the (masked) stores: ONE memory round trip.
+// (Reads issued after stores would also wait for the stores: CDNA4's vmcnt counts both in order.)
 template <int MAXF4>
 __device__ __forceinline__ void store_rows_rmw(float* g, const float* slab, int cnt, bool accumulate, int lane) {
-  constexpr int IT = (MAXF4 + 127) / 128;   // float4s per lane per half
+  constexpr int IT = (MAXF4 + 63) / 64;   // float4s per lane
   const int n4 = cnt / 4;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(g, (int64_t)cnt * 4);
+  f32x4_t buf[IT];
+  if (accumulate) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    f32x4_t buf[IT];
+    for (int j = 0; j < IT; ++j)
+      buf[j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * j) * 16, 0, 0));
+  } else {
 #pragma unroll
-    for (int j = 0; j < IT; ++j) {
-      const int i = lane + 64 * (j + half * IT);
-      buf[j] = reinterpret_cast<const f32x4_t*>(slab)[i < n4 ? i : n4 - 1];
-      if (accumulate)
-        buf[j] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, i * 16, 0, 0));
-    }
+    for (int j = 0; j < IT; ++j) buf[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
-    for (int j = 0; j < IT; ++j) {
-      const int i = lane + 64 * (j + half * IT);
-      if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
-    }
+  for (int j = 0; j < IT; ++j) {
+    const int i = lane + 64 * j;
+    buf[j] += reinterpret_cast<const f32x4_t*>(slab)[i < n4 ? i : n4 - 1];
+  }
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int i = lane + 64 * j;
+    if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
   }
 }
 

@@ -138,10 +138,13 @@ def test_self_attention_f16_form(cuda, case):
         q[0, 7, :d] = 250.0             # entry 0, head 0, query 7: c q ~ 57
         k[0, 1500, :d] = 250.0          # key 1500 (tile 5): c s ~ 5.7e5, tile 0 stays ordinary
     if case == "multi_late_peak":
-        # K < 256: the F16 multi-block kernel (128-key tiles); tile 0 ordinary, key 150 (tile 1)
-        # with in-range q and k but c s ~ 5.7e5 > 65504: the recompute must take the exact path
-        q[0, 7, :d] = 250.0
-        k[0, 150, :d] = 250.0
+        # K < 256: the F16 multi-block kernel (one masked 256-key tile, per-sub-block reference
+        # point); query 7's logits stay ordinary until key 150 (sub-block 4), where c q (~456) and
+        # k (10) are inside the f16 range but c s ~ 1.8e5 > 65504: the recompute must take the
+        # exact path.  (k is kept moderate: the F16 form's logit error grows with |c q| |k|, and a
+        # large k would also perturb every other row -- that is the form's documented bound)
+        q[0, 7, :d] = 2000.0
+        k[0, 150, :d] = 10.0
     src = [0, 0] if case == "remap" else None
     o = torch.empty_like(q)
     _hip.self_attn(q, k, v, o, H, d ** -0.5, compute="bf16", qk_src=src)

@@ -17,11 +17,13 @@ from p2p_amd import _hip, programs, seq_aligner  # noqa: E402
 from p2p_amd import pipeline as pl  # noqa: E402
 from p2p_amd.tokenizer import default_tokenizer  # noqa: E402
 
-NWG, W, SLOTS = 4096, 4, 16
+NWG, W, SLOTS = 4096, 4, 24
 PLAIN = [(0, 1, "loads issued"), (1, 2, "LDS staged + barrier"), (2, 3, "QK + softmax"), (3, 4, "PV"),
          (4, 5, "O store")]
 EDIT = [(0, 8, "src stage + barrier"), (8, 9, "P0"), (9, 10, "R = P0 M + barrier"), (10, 11, "own stage + barrier"),
-        (11, 12, "own QK + softmax"), (12, 13, "blend"), (13, 14, "store epilogue"), (14, 15, "PV")]
+        (11, 12, "own QK + softmax"), (12, 13, "blend"), (13, 14, "store epilogue"), (14, 15, "PV"),
+        (13, 16, "  store: sync + slab write"), (16, 17, "  store: sync"), (17, 18, "  store: blend sums"),
+        (18, 14, "  store: read-add-write")]
 
 
 def run(name, P, d, store, blend):
