@@ -1095,10 +1095,21 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.N), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v),
                "s"(a.o), "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv),
                "s"(a.bso), "s"(a.scale_log2));
-  const int qt = logical % a.n_qtiles;
-  const int rest = logical / a.n_qtiles;
-  const int h = rest % a.H;
-  const int n = a.N - 1 - rest / a.H;  // the edits sit last in the batch: dispatch them first
+  // heads fastest (whole q / o lines per XCD, as in cross_group_kernel)
+  int qt, h, rest;
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 126) {   // A/B: query tiles fastest (the previous order)
+    qt = logical % a.n_qtiles;
+    h = (logical / a.n_qtiles) % a.H;
+    rest = logical / a.n_qtiles / a.H;
+  } else
+#endif
+  {
+    h = logical % a.H;
+    qt = (logical / a.H) % a.n_qtiles;
+    rest = logical / a.H / a.n_qtiles;
+  }
+  const int n = a.N - 1 - rest;  // the edits sit last in the batch: dispatch them first
   // one dependent kernel-argument load decides the path (every a.field read is a scalar memory
   // round trip; chains of them cost ~1 us at the start of every workgroup)
   const int info = a.ent_info[n];

@@ -79,10 +79,23 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, EDIT, STORE>())) void c
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   P2P_GROUP_STAMP(0)
-  const int qt = logical % a.n_qtiles;
-  const int rest = logical / a.n_qtiles;
-  const int h = rest % a.H;
-  const int gi = a.n_groups - 1 - rest / a.H;   // edit groups sit last: dispatch them first
+  // heads fastest: the 8 heads of one query tile run side by side on one XCD (xcd_remap keeps
+  // consecutive logical ids together), so the 640-byte q / o rows they share leave and enter that
+  // XCD's L2 as whole lines instead of 80-byte pieces fetched and merged per head
+  int qt, h, rest;
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 126) {   // A/B: query tiles fastest (the previous order)
+    qt = logical % a.n_qtiles;
+    h = (logical / a.n_qtiles) % a.H;
+    rest = logical / a.n_qtiles / a.H;
+  } else
+#endif
+  {
+    h = logical % a.H;
+    qt = (logical / a.H) % a.n_qtiles;
+    rest = logical / a.H / a.n_qtiles;
+  }
+  const int gi = a.n_groups - 1 - rest;   // edit groups sit last: dispatch them first
   const int first = a.grp_first[gi];
   const int count = a.grp_count[gi];
   const char* const prog = static_cast<const char*>(a.grp_prog[gi]);

@@ -57,7 +57,7 @@ def run(name, P, d, store, blend):
     nq = (P + 127) // 128
     nwg = nq * H * N
     s = s[:nwg]
-    ent = N - 1 - (np.arange(nwg) // nq) // H
+    ent = N - 1 - np.arange(nwg) // (nq * H)      # heads fastest, then query tiles
     t0 = s[:, :, 0]
     print(f"== {name}: P={P} d={d} store={store} blend={blend}: {nwg} workgroups")
     plain = ent < B + 1 if not store else ent < B

@@ -48,7 +48,7 @@ def run(name, P, d, store):
     nq = (P + 127) // 128
     nwg = min(NWG, nq * H * 2)
     s = s[:nwg]
-    gi = 1 - (np.arange(nwg) // nq) // H            # group index (cond group dispatched first)
+    gi = 1 - np.arange(nwg) // (nq * H)             # group index (cond group first; heads fastest)
     print(f"== {name}: P={P} d={d} store={store}: {nwg} workgroups")
     for label, sel in (("edit group", gi == 1), ("uncond group", gi == 0)):
         ss = s[sel]
