@@ -42,13 +42,14 @@ __device__ unsigned long long g_group_stamps[2048 * 4 * 24];
 
 // two workgroups per CU (<= 256 VGPRs) where the state fits without spills: d = 40 unless it both
 // edits and stores, d = 80 plain; the others take one (their grids are <= 128 workgroups anyway)
-template <int D, bool EDIT, bool STORE>
+template <int D, int W, bool EDIT, bool STORE>
 constexpr int group_occupancy() {
+  if (W >= 8) return 1;   // 8 waves: two per SIMD already
   return (D <= 40 && !(EDIT && STORE)) || (D <= 80 && !EDIT && !STORE) ? 2 : 1;
 }
 
 template <int D, int W, bool EDIT, bool STORE>
-__global__ __launch_bounds__(64 * W, (group_occupancy<D, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
+__global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   constexpr int NKT = DK / 16;
@@ -487,7 +488,13 @@ bool cross_group_eligible(const CrossArgs& a, int d) {
 
 int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
+#ifdef P2P_EXPERIMENTS
+    case 40:
+      if (a.variant == 127) return (int)launch_group<40, 8>(a, st);   // A/B: 8-wave workgroups
+      return (int)launch_group<40, 4>(a, st);
+#else
     case 40: return (int)launch_group<40, 4>(a, st);
+#endif
     case 80: return (int)launch_group<80, 4>(a, st);
     case 160: return (int)launch_group<160, 4>(a, st);
     default: return P2P_E_HEAD_DIM;

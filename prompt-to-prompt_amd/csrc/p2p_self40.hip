@@ -141,10 +141,18 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 #endif
   };
   stamp(0);
-  const int qt = logical % a.n_qtiles;
-  const int nh = logical / a.n_qtiles;
-  const int h = nh % a.H;
-  const int n = nh / a.H;
+  // FORM bit 8192: heads fastest -- one XCD then runs all heads of a query tile (whole q / o lines
+  // in its L2) and, with xcd_remap's contiguous chunks, all tiles of one entry (its K / V once)
+  int qt, h, n;
+  if constexpr ((FORM & 8192) != 0) {
+    h = logical % a.H;
+    qt = (logical / a.H) % a.n_qtiles;
+    n = logical / a.H / a.n_qtiles;
+  } else {
+    qt = logical % a.n_qtiles;
+    h = (logical / a.n_qtiles) % a.H;
+    n = logical / a.n_qtiles / a.H;
+  }
   const int src = a.qk_src[n];
   const int pw = (qt * WAVES + wave) * 32 * QB;   // first query of this wave
   const int K = a.K;
@@ -663,6 +671,7 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
       case 101: return (int)launch<80, 8, 1, 64, true, 1>(a, st);
       case 102: return (int)launch<80, 8, 1, 128, true, 1>(a, st);
       case 103: return (int)launch<80, 4, 2, 128, true, 1 | 16>(a, st);   // 92 with clock stamps
+      case 128: return (int)launch<80, 4, 2, 128, true, 1 | 8192>(a, st);  // default, heads fastest
 #endif
       default: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
     }
@@ -695,6 +704,7 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 105: return (int)launch<40, 4, 2, 128, true, 1 | 128 | 4096>(a, st);
     case 106: return (int)launch<40, 4, 2, 64, true, 1 | 4096>(a, st);
     case 107: return (int)launch<40, 4, 2, 128, true, 1 | 16 | 4096>(a, st);   // 104 with clock stamps
+    case 128: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 8192>(a, st);   // default, heads fastest
 #endif
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // alternate step pairs: G1 0.1931-0.1938 ms vs 0.1964 (66) and 0.2056 (round 2), profiles/r03
