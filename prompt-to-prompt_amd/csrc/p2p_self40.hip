@@ -212,7 +212,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // K and V of the chunk; split staging: role 1 = K chunks of threads 0..NT/2-1, role 2 = V
   // chunks of the others, each thread holding SCH of them in kreg)
   const bool young = __builtin_amdgcn_readfirstlane(wave) >= WAVES / 2;
-  const int stid = kSplit ? tid - (young ? NT / 2 : 0) : tid;
+  // FORM bit 65536: the roles of the two halves swapped (the younger half converts K)
+  const bool vrole = ((FORM & 65536) != 0) ? !young : young;
+  const int stid = kSplit ? tid - (young ? NT / 2 : 0) : tid;   // (position within the half)
   const int sstride = kSplit ? NT / 2 : NT;
   short8_t kreg[CMAX], vreg[NCH];
   uint32_t koff[CMAX], voff[NCH];
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     const int ch = cidx - (cidx / kCPR) * kCPR;
     lrow[i] = row;
     lch[i] = ch;
-    koff[i] = (uint32_t)((row * (int)(kSplit && young ? a.ldv : a.ldk) + ch * 8) * 2);
+    koff[i] = (uint32_t)((row * (int)(kSplit && vrole ? a.ldv : a.ldk) + ch * 8) * 2);
     if (i < NCH) voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
   }
   const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + kD) * 2;
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       for (int i = 0; i < nchunks(role); ++i) stage_write(i, buf, as_f16, role);
     };
     if constexpr (!kSplit) go(std::integral_constant<int, 0>{});
-    else if (young) go(std::integral_constant<int, 2>{});
+    else if (vrole) go(std::integral_constant<int, 2>{});
     else go(std::integral_constant<int, 1>{});
   };
 
@@ -412,10 +414,12 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
         if (young) __builtin_amdgcn_s_setprio(0);
       // FORM bit 256: the younger half holds priority 1 for the first half of every kAlt steps
       // (bit 512: kAlt = 4, else 2), so the two waves of a SIMD share the VALU evenly
+      // (bits 16384 / 32768, with 512: priority 1 for 3 of every 4 steps / 1 of every 4)
       if constexpr ((FORM & 256) != 0) {
         constexpr int kAlt = (FORM & 512) ? 4 : 2;
+        constexpr int kOn = (FORM & 16384) ? 3 : (FORM & 32768) ? 1 : kAlt / 2;
         if constexpr (x % kAlt == 0) { if (young) __builtin_amdgcn_s_setprio(1); }
-        if constexpr (x % kAlt == kAlt / 2) { if (young) __builtin_amdgcn_s_setprio(0); }
+        if constexpr (x % kAlt == kOn) { if (young) __builtin_amdgcn_s_setprio(0); }
       }
       constexpr int sb = x / QB, b = x % QB;
       // K of sub-block sb+1: LEAN after this step's Q K^T when it was the last one on sb
@@ -522,7 +526,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     else tile(ntiles - 1, kNo, kYes, role);
   };
   if constexpr (!kSplit) run_tiles(std::integral_constant<int, 0>{});
-  else if (young) run_tiles(std::integral_constant<int, 2>{});
+  else if (vrole) run_tiles(std::integral_constant<int, 2>{});
   else run_tiles(std::integral_constant<int, 1>{});
 
   {
@@ -705,10 +709,16 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 106: return (int)launch<40, 4, 2, 64, true, 1 | 4096>(a, st);
     case 107: return (int)launch<40, 4, 2, 128, true, 1 | 16 | 4096>(a, st);   // 104 with clock stamps
     case 128: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 8192>(a, st);   // default, heads fastest
+    case 129: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // young prio 3/4 of steps
+    case 130: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 32768>(a, st);   // young prio 1/4
+    case 131: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 65536>(a, st);         // young half converts K
+    case 132: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 65536>(a, st);               // swap, no priority
 #endif
+    case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
-    // alternate step pairs: G1 0.1931-0.1938 ms vs 0.1964 (66) and 0.2056 (round 2), profiles/r03
-    default: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);
+    // three of every four steps: G1 0.1867 ms vs 0.1880-0.1885 for priority on alternate step pairs
+    // (133) and 0.2056 for round 2 (profiles/r03/g1_ab/r03y_ab.log)
+    default: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);
   }
 #endif
 }
