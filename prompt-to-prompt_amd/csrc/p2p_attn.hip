@@ -1733,6 +1733,7 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     // waves of a 32-query workgroup split the keys (p2p_selfsplit.hip); variant 121 (experiments
     // build) keeps the per-tile kernel below for A/B timing
     if (mode == MODE_FUSED && self_split_eligible(a, D) && a.variant != 121) return (hipError_t)run_self_split(a, D, st);
+    if (mode == MODE_FUSED && self_ring_eligible(a, D) && a.variant != 134) return (hipError_t)run_self_ring(a, D, st);
   }
   if (mode == MODE_FUSED) {
     // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)

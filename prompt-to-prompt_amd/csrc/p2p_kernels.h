@@ -86,6 +86,9 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st);
 // d = 160 self-attention with bf16 inputs, O only, K <= 256 (p2p_selfsplit.hip): key-split waves
 bool self_split_eligible(const SelfArgs& a, int d);
 int run_self_split(const SelfArgs& a, int d, hipStream_t st);
+// d = 160 self-attention with bf16 inputs, O only, K > 128: 4-stage global_load_lds ring
+bool self_ring_eligible(const SelfArgs& a, int d);
+int run_self_ring(const SelfArgs& a, int d, hipStream_t st);
 int run_localblend(const p2p_blend_args& a, hipStream_t st);
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st);
 

@@ -178,6 +178,158 @@ __global__ __launch_bounds__(64 * W, 2) void self_split_kernel(SelfArgs a) {
   }
 }
 
+// d = 160 with more keys (the 16x16 layers: P = K = 256): one workgroup = 128 queries (4 waves x
+// 32) of one (entry, head), 32-key tiles through a 4-stage LDS ring filled by global_load_lds DMA
+// (no VGPRs), three tiles in flight: the per-tile kernel's one-tile-ahead register prefetch left
+// every 32-key tile waiting on its own round trip.  Each wave issues exactly 6 DMA instructions per
+// tile (3 K, 3 V; slots past the tile fetch a harmless chunk), so "tile kt has landed" is the
+// counted wait vmcnt(12) (tiles kt+1, kt+2 still in flight), then one barrier per tile.  K rows
+// sit at 21 16-byte slots (336 B: the b128 fragment reads of 16 rows hit 16 bank slots; slot 20 is
+// padding), V rows at 20 (320 B, conflict-free for the transposed reads).  Online softmax with the
+// defer-max rule, f32 row sums; the output leaves through LDS as whole 16-byte row chunks.
+constexpr int kRingStages = 4;
+
+// One global_load_lds_dwordx4 (16 bytes per lane into LDS at lds_off + lane * 16), as inline asm
+// so hipcc does not track it: its own bookkeeping would drain every in-flight DMA with vmcnt(0)
+// before the next LDS read of the ring (it cannot tell the stages apart).  The ring's waits are
+// the explicit counted vmcnt below; the compiler's own waits only grow stricter with these newer
+// operations in the in-order counter.  (cdna_hip_programming.md, the m0 recipe.)
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_off) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_off)
+               : "memory");
+}
+constexpr int kRingStageBytes = 2 * 12 * 1024;   // K: 12 DMA instructions x 1 KiB, V: the same
+
+template <int D, int W>
+__global__ __launch_bounds__(64 * W, 1) void self_ring_kernel(SelfArgs a) {
+  static_assert(D == 160, "the slot layout below is for d = 160");
+  static_assert(W == 1 || W == 2 || W == 4, "24 DMA instructions per tile split evenly");
+  constexpr int kPer = 12 / W;          // K (and V) DMA instructions per wave per tile
+  constexpr int kWait = 2 * 2 * kPer;   // this wave's DMAs of two tiles still in flight
+  constexpr int NKT = D / 16, NDT = D / 32, KCH = D / 8, KSL = KCH + 1;
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char ring[kRingStages * kRingStageBytes];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, qi = lane & 31;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H, n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int K = a.K;
+  const float c = a.scale_log2;
+  const int p = qt * 32 * W + wave * 32 + qi;
+  const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * D;
+
+  short8_t qf[NKT];
+  {
+    const int pr = min(p, a.P - 1);   // rows past P: any valid row, never stored
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) qf[t] = *reinterpret_cast<const short8_t*>(qp + (int64_t)pr * a.ldq + 16 * t + 8 * hh);
+  }
+  // Q retired before any DMA is in flight: hipcc then knows it complete, and its waits inside the
+  // loop cannot end up counting (and draining) the ring
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  const int ntiles = (K + 31) / 32;
+  // this wave's 3 K and 3 V DMA instructions of tile kt into stage kt % kRingStages
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)ring;
+  auto issue = [&](int kt) __attribute__((always_inline)) {
+    const uint32_t st = __builtin_amdgcn_readfirstlane(ring_lds + (kt % kRingStages) * kRingStageBytes);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = wave * kPer + j;              // instruction 0..11 of the tile
+      const int slot = i * 64 + lane;
+      int row = slot / KSL, ch = slot - row * KSL;
+      if (ch >= KCH || row >= 32) { row = 0; ch = 0; }   // padding slot: fetch any valid chunk
+      const int key = min(kt * 32 + row, K - 1);
+      glds16(kp + (int64_t)key * a.ldk + ch * 8, __builtin_amdgcn_readfirstlane(st + i * 1024));
+      int vrow = slot / KCH, vch = slot - vrow * KCH;
+      if (vrow >= 32) { vrow = 0; vch = 0; }
+      const int vkey = min(kt * 32 + vrow, K - 1);
+      glds16(vp + (int64_t)vkey * a.ldv + vch * 8, __builtin_amdgcn_readfirstlane(st + 12 * 1024 + i * 1024));
+    }
+  };
+  // three tiles in flight (tiles past the last re-fetch the last one: the counted waits stay uniform)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) issue(min(j, ntiles - 1));
+
+  f32x16_t O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    // vmcnt(kWait): this wave's DMAs of tile kt landed (tiles kt+1, kt+2 still in flight)
+    __builtin_amdgcn_s_waitcnt((0x0F70 | (kWait & 15)) | ((kWait >> 4) << 14));
+    __syncthreads();                           // ... and every other wave's
+    const char* const st = ring + (kt % kRingStages) * kRingStageBytes;
+    const uint16_t* const Kt = reinterpret_cast<const uint16_t*>(st);
+    const uint16_t* const Vt = reinterpret_cast<const uint16_t*>(st + 12 * 1024);
+    f32x16_t acc = {};
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const short8_t kf = *reinterpret_cast<const short8_t*>(Kt + (qi * KSL + 2 * t + hh) * 8);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf),
+                                                    __builtin_bit_cast(bf16x8_t, qf[t]), acc, 0, 0, 0);
+    }
+    // the stage read two tiles ago is free for tile kt + 3 once every wave passed this barrier
+    issue(min(kt + 3, ntiles - 1));
+    float sv[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sv[r] = (kt * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
+      mx = fmaxf(mx, sv[r]);
+    }
+    mx = fmaxf(mx, other_half(mx)) * c;
+    if (!__all(mx <= m_run + kThr)) {
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - mnew);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+      l_run *= alpha;
+      m_run = mnew;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sv[r] = fast_exp2(fmaf(sv[r], c, -m_run));
+      l_run += sv[r];
+    }
+    pv_block<D, NDT>(MmaBf16{}, O, Vt, 0, sv, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the trailing re-fetches retired
+  __syncthreads();                      // every wave is done with the ring
+  const float inv = 1.f / (l_run + other_half(l_run));
+  // epilogue through LDS: wave w's 32 rows at ring + w * 32 * (D + 8) * 2, then 16-byte row chunks
+  constexpr int OS = D + 8;
+  uint16_t* const orow = reinterpret_cast<uint16_t*>(ring) + wave * 32 * OS;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      store4(orow + qi * OS + dt * 32 + 8 * g + 4 * hh, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv,
+             O[dt][4 * g + 2] * inv, O[dt][4 * g + 3] * inv);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint16_t* const obase = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D;
+#pragma unroll
+  for (int c0 = 0; c0 < 32 * KCH; c0 += 64) {
+    const int cidx = c0 + lane;
+    const int row = cidx / KCH, ch = cidx - row * KCH;
+    const int pr = qt * 32 * W + wave * 32 + row;
+    if (pr < a.P)
+      *reinterpret_cast<short8_t*>(obase + (int64_t)pr * a.ldo + ch * 8) =
+          *reinterpret_cast<const short8_t*>(orow + row * OS + ch * 8);
+  }
+}
+
 template <int D, int W, int KBW>
 hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
@@ -187,7 +339,31 @@ hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int W>
+hipError_t launch_ring(const SelfArgs& a, hipStream_t st) {
+  SelfArgs b = a;
+  b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+  hipLaunchKernelGGL((self_ring_kernel<160, W>), grid, block, 0, st, b);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// d = 160, bf16 inputs, O only, K > 128: the 4-stage DMA ring (variant 134 of an experiments
+// build: the per-tile kernel of p2p_attn.hip instead)
+bool self_ring_eligible(const SelfArgs& a, int d) {
+  return d == 160 && a.K > 128 && a.lse == nullptr && a.n_maps == 0;
+}
+
+int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
+  (void)d;
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 135) return (int)launch_ring<2>(a, st);
+  if (a.variant == 136) return (int)launch_ring<1>(a, st);
+#endif
+  return (int)launch_ring<4>(a, st);
+}
 
 // d = 160, bf16 inputs, O only, K <= 128 (the 8x8 layers): the waves split the keys (W =
 // ceil(K / 64) waves of 64 keys, or 2 x 32 for K <= 64).  Measured against the per-tile kernel

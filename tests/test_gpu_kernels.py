@@ -374,10 +374,11 @@ def test_cross_group_kernel_bf16(cuda, geom, n_groups):
 
 @pytest.mark.parametrize("case", ["g3", "g4", "peaky32", "remap", "ragged", "k200", "k33", "k20"])
 def test_self_attention_key_split_d160(cuda, case):
-    """d = 160 with bf16 inputs, O only: K <= 128 takes the key-split kernel (p2p_selfsplit.hip: the
+    """d = 160 with bf16 inputs, O only (p2p_selfsplit.hip): K <= 128 takes the key-split kernel (the
     waves of a 32-query workgroup split the keys and combine (O_w, m_w, l_w) in LDS), larger K the
-    per-tile kernel.  g4 / g3: the config-2 8x8 and 16x16 launches; ragged P / K and key-split wave
-    counts 1 and 2 (K = 20, 33, 77); K = 200 and 256 on the per-tile path."""
+    4-stage DMA ring kernel.  g4 / g3: the config-2 8x8 and 16x16 launches; ragged P / K, key-split
+    wave counts 1 and 2 (K = 20, 33, 77), K = 200 (a partial last ring tile), peaky rows (defer-max
+    rescales), a source remap."""
     N, P, K, H, d = {"g3": (8, 256, 256, 8, 160), "g4": (8, 64, 64, 8, 160), "ragged": (3, 100, 77, 2, 160),
                      "k200": (2, 130, 200, 4, 160), "k33": (2, 70, 33, 2, 160),
                      "k20": (2, 45, 20, 2, 160)}.get(case, (4, 256, 256, 4, 160))
