@@ -269,13 +269,16 @@ __global__ __launch_bounds__(64 * W, 1) void self_ring_kernel(SelfArgs a) {
     const char* const st = ring + (kt % kRingStages) * kRingStageBytes;
     const uint16_t* const Kt = reinterpret_cast<const uint16_t*>(st);
     const uint16_t* const Vt = reinterpret_cast<const uint16_t*>(st + 12 * 1024);
-    f32x16_t acc = {};
+    // Q K^T as two independent accumulator chains (even / odd k steps): one wave per SIMD has no
+    // partner to hide a 10-deep dependent MFMA chain behind
+    f32x16_t acc2[2] = {f32x16_t{}, f32x16_t{}};
 #pragma unroll
     for (int t = 0; t < NKT; ++t) {
       const short8_t kf = *reinterpret_cast<const short8_t*>(Kt + (qi * KSL + 2 * t + hh) * 8);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf),
-                                                    __builtin_bit_cast(bf16x8_t, qf[t]), acc, 0, 0, 0);
+      acc2[t & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf),
+                                                            __builtin_bit_cast(bf16x8_t, qf[t]), acc2[t & 1], 0, 0, 0);
     }
+    const f32x16_t acc = acc2[0] + acc2[1];
     // the stage read two tiles ago is free for tile kt + 3 once every wave passed this barrier
     issue(min(kt + 3, ntiles - 1));
     float sv[16];
