@@ -82,6 +82,16 @@ class LaunchTimer:
             self.rec.setdefault(name, []).append((start, ev, work))
             self._pending = None
 
+    def before_aux(self, name, nbytes):
+        """The LocalBlend mask and latent-step launches (HBM-type helpers), with their bytes."""
+        if self.enabled:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._pending = (name, ev, float(nbytes))
+
+    def after_aux(self, name):
+        self.after(name, None)
+
     def summary(self, name="dominant"):
         """(average ms per launch, average work per launch, launches)"""
         torch.cuda.synchronize()
@@ -96,8 +106,13 @@ class LaunchTimer:
         labels = {"cross_store_p1024": "cross_attn_kernel G2/G6 (P=1024, d=80, K=77) with the kept cross maps "
                                        "(read-add-write) + LocalBlend word sums",
                   "self_store_p1024": "self-attention G2/G6 (P=K=1024, d=80) with the kept self maps: fused "
-                                      "pass (lse) + self_maps_kernel read-add-write"}
-        for name in ("cross_store_p1024", "self_store_p1024"):
+                                      "pass (lse) + self_maps_kernel read-add-write",
+                  "localblend": "LocalBlend mask (blend_finalize_kernel: folded word sums -> pooled, thresholded "
+                                "64x64 mask)",
+                  "latent_step": "latent_step_kernel (CFG + DDIM + LocalBlend blend)"}
+        rules = {"localblend": "word sums read (B x 2 x L*H x 16^2 f32) + mask written (B x 64^2 u8)",
+                 "latent_step": "eps read (2B x 4 x 64^2, bf16) + latents read and written (f32) + mask read"}
+        for name in ("cross_store_p1024", "self_store_p1024", "localblend", "latent_step"):
             avg_ms, nbytes, n = self.summary(name)
             if not n:
                 continue
@@ -105,7 +120,8 @@ class LaunchTimer:
             out.append({"kernel": labels[name], "avg_launch_ms": avg_ms, "launches": n,
                         "algorithmic_bytes": nbytes, "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": gbps / HBM_PEAK_GBPS,
-                        "bytes_rule": "q + o + k + v (io dtype) + kept maps f32 x2 (read + write, steps >= 1)"})
+                        "bytes_rule": rules.get(name, "q + o + k + v (io dtype) + kept maps f32 x2 (read + write, "
+                                                      "steps >= 1)")})
         return out
 
 

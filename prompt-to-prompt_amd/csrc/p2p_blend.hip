@@ -98,16 +98,19 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
     const float* wa = a.word_sums + (int64_t)(bb * 2 + 0) * LH * R2 + pix;
     const float* ws = a.word_sums + (int64_t)(bb * 2 + 1) * LH * R2 + pix;
     float sa = 0.f, ss = 0.f;
-    for (int j0 = 0; j0 < LH; j0 += 16) {   // 32 loads in flight, then the in-order sums
-      float va[16], vs[16];
+    // every load in flight at once (the five blended 16x16 layers x 8 heads = 40 maps: one memory
+    // round trip instead of three), then the in-order sums
+    constexpr int kBatch = 48;
+    for (int j0 = 0; j0 < LH; j0 += kBatch) {
+      float va[kBatch], vs[kBatch];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
+      for (int u = 0; u < kBatch; ++u) {
         const int j = min(j0 + u, LH - 1);
         va[u] = wa[(int64_t)j * R2];
         vs[u] = ws[(int64_t)j * R2];
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
+      for (int u = 0; u < kBatch; ++u)
         if (j0 + u < LH) {
           sa += va[u];
           ss += vs[u];

@@ -320,7 +320,16 @@ def localblend(maps, heads_per_map, alpha_layers, substruct_layers, th_pool, th_
     a.word_sums = word_sums.data_ptr()
     a.mask_out = mask_out.data_ptr() if mask_out is not None else None
     a.word_sums_ready = int(bool(word_sums_ready))
+    obs = LAUNCH_OBSERVER
+    if obs is not None and hasattr(obs, "before_aux"):
+        # algorithmic bytes: the word sums (or the maps) read, the mask written, x_t read + written
+        LH, R2 = len(maps) * heads_per_map, a.map_res * a.map_res
+        nbytes = (B * 2 * LH * R2 * 4 if word_sums_ready else sum(m.numel() * 4 for m in maps) + B * 2 * LH * R2 * 8)
+        nbytes += B * a.lat_h * a.lat_w + (2 * x_t.numel() * 4 if x_t is not None else 0)
+        obs.before_aux("localblend", nbytes)
     rc = lib().p2p_localblend(ctypes.byref(a), _stream((x_t if x_t is not None else mask_out).device))
+    if obs is not None and hasattr(obs, "after_aux"):
+        obs.after_aux("localblend")
     _check(rc, "p2p_localblend")
 
 
@@ -364,7 +373,14 @@ def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, gro
         a.group_blend = group_blend.data_ptr()
     else:
         a.group_blend = None
+    obs = LAUNCH_OBSERVER
+    if obs is not None and hasattr(obs, "before_aux"):
+        # algorithmic bytes: eps read, x read, out written, mask read
+        obs.before_aux("latent_step", eps.numel() * eps.element_size() + 2 * x.numel() * 4 +
+                       (mask.numel() if mask is not None else 0))
     rc = lib().p2p_latent_step(ctypes.byref(a), _stream(x.device))
+    if obs is not None and hasattr(obs, "after_aux"):
+        obs.after_aux("latent_step")
     _check(rc, "p2p_latent_step")
     return out
 
