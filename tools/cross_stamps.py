@@ -61,7 +61,9 @@ def run(name, P, d, store, blend):
     t0 = s[:, :, 0]
     print(f"== {name}: P={P} d={d} store={store} blend={blend}: {nwg} workgroups")
     plain = ent < B + 1 if not store else ent < B
-    for label, sel, phases in (("plain", plain, PLAIN), ("edit", ~plain, EDIT)):
+    src = (ent == B) & ~plain
+    edit = ent > B
+    for label, sel, phases in (("plain", plain, PLAIN), ("source", src, EDIT), ("edit", edit, EDIT)):
         ss = s[sel]
         if not len(ss):
             continue
