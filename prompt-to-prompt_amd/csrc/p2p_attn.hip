@@ -1058,7 +1058,7 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #endif
 
 template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
-__global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_attn_kernel(CrossArgs a) {
+__global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
   constexpr int DK = (D + 15) / 16 * 16;
@@ -1397,6 +1397,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   const bool dense = kDenseOk && edit;   // the launcher picks DENSE only if every edit group is
   f32x16_t Rd[KB];
   int dense_flags = 3;   // dense edits: the blend halves in use (set from the coefficients)
+  // dense edits: this entry's own K / V are loaded together with the source's prologue loads, so
+  // the workgroup waits one memory round trip instead of two (variant 138 of an experiments
+  // build: own K / V staged after the R phase, as before)
+  Chunk8<IO> kc1[kDenseOk ? NCH : 1], vc1[kDenseOk ? NCH : 1];
+  bool own_early = false;
   if constexpr (kDenseOk) {
    if (dense) {
     const uint16_t* mg = static_cast<const uint16_t*>(a.grp_dense[gi]) +
@@ -1426,6 +1431,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
     Chunk8<IO> kc0[NCH], vc0[NCH];
     load_kv(first, kc0, vc0, false);
     load_q(first, qf);
+    own_early = true;
+#ifdef P2P_EXPERIMENTS
+    if (a.variant == 138) own_early = false;
+#endif
+    if (own_early) load_kv(n, kc1, vc1, true);
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const int i = tid + j * NT;
@@ -1505,7 +1515,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 3 : 1) void cross_
   } else if (!edit) {
     load_q(n, qf);
   }
-  stage(n, true);
+  if constexpr (kDenseOk) {
+    if (own_early) store_kv(kc1, vc1, true);
+    else stage(n, true);
+  } else {
+    stage(n, true);
+  }
   __syncthreads();
   P2P_CROSS_STAMP(11)
   if (!dense || (dense_flags & 1)) {
