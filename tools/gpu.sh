@@ -14,6 +14,10 @@
 #     pmc:<name>:<counters>  one rocprofv3 --pmc pass (comma-separated counters) over tools/g1_only.py
 #                            (G1 launches only; P2P_SELF_VARIANT / P2P_EXPERIMENTS_LIB from the env)
 #     cross                  tools/cross_bench.py (cross-attention launch shapes)
+#     crossab:<v1,v2,..>     tools/cross_bench.py in graph mode, one process per P2P_SELF_VARIANT (experiments lib)
+#     smallab:<v1,v2,..>     tools/small_bench.py (G2/G3/G4 self-attention), one process per variant
+#     stamps:<tool>:<v>      a clock-stamp tool (tools/<tool>.py) under P2P_SELF_VARIANT=v (experiments lib)
+#     pmcs:<tag>:<script>:<args>  tools/gpu_pmc.sh over any launcher script (comma-separated args)
 #     py:<script>[:<args>]   python -u <script> <args>
 set -u
 export TMPDIR=/tmp
@@ -53,6 +57,24 @@ for step in "$@"; do
       f=$(find "$out/pmc_$name" -name "*counter_collection.csv" | head -1)
       [ -n "$f" ] && python3 tools/pmc_summary.py "$f" | tee -a "$out/pmc_summary.txt" ;;
     cross) run 600 "$out/cross.log" python -u tools/cross_bench.py; tail -20 "$out/cross.log" ;;
+    crossab)
+      for v in ${arg//,/ }; do
+        run 300 "$out/cross_v$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v CROSS_BENCH_GRAPH=1 python -u tools/cross_bench.py
+        echo "cross v$v"; grep '^{' "$out/cross_v$v.log"
+      done ;;
+    smallab)
+      for v in ${arg//,/ }; do
+        run 200 "$out/small_v$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v python -u tools/small_bench.py
+        grep '^{' "$out/small_v$v.log"
+      done ;;
+    stamps)
+      tool=${arg%%:*}; v=${arg#*:}
+      run 200 "$out/${tool}_v$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v python -u tools/$tool.py
+      grep -v '^$' "$out/${tool}_v$v.log" | tail -20 ;;
+    pmcs)
+      ptag=${arg%%:*}; rest=${arg#*:}; script=${rest%%:*}; sargs=${rest#*:}
+      PMC_SCRIPT=$script run 600 "$out/pmc_$ptag.log" bash tools/gpu_pmc.sh "$ptag" ${sargs//,/ }
+      grep -E "p2p.*(FETCH_SIZE|WRITE_SIZE)" gpurun_out/pmc/${ptag}_summary.txt || true ;;
     py)
       script=${arg%%:*}; sargs=""; [ "$script" != "$arg" ] && sargs=${arg#*:}
       run 1100 "$out/py_$(basename "$script" .py).log" python -u "$script" $sargs
