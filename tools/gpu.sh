@@ -50,7 +50,9 @@ for step in "$@"; do
     prof)
       run 900 "$out/prof.log" rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 -u bench.py $arg
       grep '^{' "$out/prof.log" | tail -1 | tee "$out/bench_under_rocprof.json"
-      find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \; ;;
+      find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
+      db=$(find "$out/prof" -name "*.db" | head -1)
+      if [ -n "$db" ]; then python3 tools/rocpd_summary.py "$db" > "$out/rocprof_summary.txt"; sed -n '/hot path/,$p' "$out/rocprof_summary.txt" | head -14; fi ;;
     pmc)
       name=${arg%%:*}; counters=${arg#*:}
       run 120 "$out/pmc_$name.log" timeout -s KILL 100 rocprofv3 --pmc ${counters//,/ } --output-format csv -d "$out/pmc_$name" -o run -- python3 -u tools/g1_only.py
