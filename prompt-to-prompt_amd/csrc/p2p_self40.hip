@@ -117,6 +117,15 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // when there are more chunks than steps), from the middle of the tile on -- the loads issued at
   // its start have landed by then
   constexpr int kHalf = X / 2;
+  // FORM bit 131072: the per-tile barrier split into LDS counters (tsync).  tsync[b] counts the
+  // waves that have written their chunks of a tile into buffer b, tsync[2 + b] the waves done
+  // reading a tile from it; a wave waits only for the chunks it reads next or for the readers of
+  // the buffer it overwrites, so the waves of a workgroup drift up to (X - kWe) steps apart.  The
+  // staging window moves to [X/4, X/2) (bit 262144: [X/2, 3X/4)) to leave that slack
+  constexpr bool kFlagSync = (FORM & 131072) != 0;
+  constexpr int kWs = !kFlagSync ? kHalf : (FORM & 262144) ? X / 2 : X / 4;
+  constexpr int kWe = !kFlagSync ? X : (FORM & 262144) ? (3 * X) / 4 : X / 2;
+  static_assert(kWe > kWs, "staging window");
   auto nchunks = [](auto role) { return decltype(role)::value == 0 ? NCH : SCH; };
   // K and V tile buffers; after the last tile the same LDS holds each wave's output rows (epilogue)
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KBUF + 2 * VBUF];
@@ -125,6 +134,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int kOS = kD + 8;   // output row in LDS: 16-byte aligned, rows on distinct banks
   static_assert(WAVES * 32 * QB * kOS <= 2 * KBUF + 2 * VBUF, "epilogue rows fit the tile buffers");
   __shared__ int wg_flag;
+  __shared__ int tsync[4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -175,6 +185,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
           short8_t{(short)(j == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
   }
   if (tid == 0) wg_flag = 0;
+  if constexpr (kFlagSync)
+    if (tid < 4) tsync[tid] = 0;
 
   // ---- Q fragments: lane (qi, hh) of block b, k step t holds Q[p][16t + 8hh .. +7]
   bool ovf = false;
@@ -349,6 +361,31 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int kFlipSel = (FORM >> 5) & 3;
   constexpr int kFlip = kFlipSel == 1 ? X / 2 : kFlipSel == 2 ? X / 4 : kFlipSel == 3 ? (3 * X) / 4 : 0;
   bool bad = false;
+  // tsync[idx] >= target, read by one wave-uniform LDS load per poll; a poll bound that runs out
+  // (it cannot in a correct schedule: the writer of a buffer never waits on its readers' next
+  // tile) marks the wave bad, which sends the workgroup to the barrier-synchronised exact
+  // recompute instead of hanging
+  auto tsync_wait = [&](int idx, int target) __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    int seen = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(&tsync[idx]));
+    if (__builtin_expect(seen < target, 0)) {
+      for (int spin = 0; seen < target; ++spin) {
+        if (spin >= (1 << 16)) {
+          bad = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        seen = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(&tsync[idx]));
+      }
+    }
+    asm volatile("" ::: "memory");
+  };
+  // this wave's LDS writes (or reads) of a buffer complete, then one count
+  auto tsync_signal = [&](int idx) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) atomicAdd(&tsync[idx], 1);
+    asm volatile("" ::: "memory");
+  };
   // ---- one tile of the fast form, software-pipelined over its X blocks.  more: the next tile
   // is staged during this one (compile-time, so the tile body is one basic block); masked: keys
   // past K in this tile
@@ -358,6 +395,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     constexpr int kNcw = nchunks(role);
     const int buf = kt & 1;
     if constexpr (kMore) stage_load(kt + 1, role);
+    if constexpr (kFlagSync)
+      if (kt >= 1) tsync_wait(buf, WAVES * ((kt + 1) >> 1));   // every wave's chunks of this tile
     const uint16_t* const Kb = Ks + buf * KBUF;
     const uint16_t* const Vb = Vs + buf * VBUF;
     // LEAN: one K and one V fragment set, each re-read right after its last reader (K of
@@ -410,6 +449,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     if constexpr (SCHED) __builtin_amdgcn_sched_barrier(0);
     static_for<X>([&](auto xc) __attribute__((always_inline)) {
       constexpr int x = decltype(xc)::value;
+      if constexpr (kFlagSync && kMore && x == kWs)   // every wave done with tile kt - 1 (same buffer)
+        if (kt >= 1) tsync_wait(2 + (buf ^ 1), WAVES * ((kt + 1) >> 1));
+      if constexpr (kFlagSync && kMore && x == kWe) tsync_signal(buf ^ 1);
       if constexpr (kFlip > 0 && x == kFlip)
         if (young) __builtin_amdgcn_s_setprio(0);
       // FORM bit 256: the younger half holds priority 1 for the first half of every kAlt steps
@@ -432,8 +474,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       // the next tile's chunks go to the other buffer over the second half of the tile (every
       // wave has passed the barrier that ended the tile which last read that buffer)
       // chunks [c0, c1) of this thread are written in this step
-      constexpr int c0 = x < kHalf ? 0 : ((x - kHalf) * kNcw + (X - kHalf) - 1) / (X - kHalf);
-      constexpr int c1 = x < kHalf ? 0 : ((x + 1 - kHalf) * kNcw + (X - kHalf) - 1) / (X - kHalf);
+      constexpr int kWn = kWe - kWs;
+      constexpr bool kInW = x >= kWs && x < kWe;
+      constexpr int c0 = kInW ? ((x - kWs) * kNcw + kWn - 1) / kWn : 0;
+      constexpr int c1 = kInW ? ((x + 1 - kWs) * kNcw + kWn - 1) / kWn : 0;
       constexpr bool kStw = kMore && c1 > c0;
       constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
       if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
@@ -515,7 +559,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
         }
       }
     }
-    __syncthreads();
+    if constexpr (kFlagSync) tsync_signal(2 + buf);   // this wave's reads of buf are done
+    else __syncthreads();
     stamp(3 + 2 * kt);
   };
   constexpr std::false_type kNo{};
@@ -713,6 +758,11 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 130: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 32768>(a, st);   // young prio 1/4
     case 131: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 65536>(a, st);         // young half converts K
     case 132: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 65536>(a, st);               // swap, no priority
+    // the tile barrier split into LDS counters (staging window [X/4, X/2) / [X/2, 3X/4)); 141 = 139 with stamps
+    case 139: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072>(a, st);
+    case 140: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 262144>(a, st);
+    case 141: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 16>(a, st);
+    case 142: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 131072>(a, st);   // no priority duty
 #endif
     case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
