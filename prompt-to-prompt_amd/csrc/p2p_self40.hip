@@ -106,7 +106,14 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int NCH = (BK * kCPR + NT - 1) / NT;
   constexpr int KBUF = BK * kKS;
   constexpr int VBUF = BK * kVS;
-  constexpr int X = NSB * QB;   // pipeline steps (32x32 blocks) per tile
+  // FORM bit 524288 (key split): wave w and w + WAVES/2 hold the same queries and take the two
+  // halves of every tile's keys, combined through LDS at the end -- twice the waves per SIMD for
+  // grids of one workgroup per CU without halving the reuse of each K / V fragment
+  constexpr bool kKSplit = (FORM & 524288) != 0;
+  constexpr int WQ = kKSplit ? WAVES / 2 : WAVES;   // query waves
+  constexpr int NSBW = kKSplit ? NSB / 2 : NSB;     // 32-key sub-blocks per wave and tile
+  static_assert(!kKSplit || (NSB % 2 == 0 && WAVES % 2 == 0), "key split");
+  constexpr int X = NSBW * QB;   // pipeline steps (32x32 blocks) per tile
   constexpr float kThr = 8.0f;  // exact path: defer-max threshold (log2 units)
   // FORM bit 128 (split staging): waves 0..WAVES/2-1 stage K (the f16 conversion), the younger
   // half -- the VALU-arbitration loser -- stages V (copy only); else every wave stages both
@@ -164,7 +171,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     n = logical / a.n_qtiles / a.H;
   }
   const int src = a.qk_src[n];
-  const int pw = (qt * WAVES + wave) * 32 * QB;   // first query of this wave
+  const int khalf = kKSplit ? __builtin_amdgcn_readfirstlane(wave) / WQ : 0;   // key half (key split)
+  const int wq = kKSplit ? wave - khalf * WQ : wave;
+  const int sbo = khalf * NSBW;                   // first sub-block of this wave in a tile
+  const int pw = (qt * WQ + wq) * 32 * QB;        // first query of this wave
   const int K = a.K;
   const float c = a.scale_log2;
 
@@ -397,8 +407,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     if constexpr (kMore) stage_load(kt + 1, role);
     if constexpr (kFlagSync)
       if (kt >= 1) tsync_wait(buf, WAVES * ((kt + 1) >> 1));   // every wave's chunks of this tile
-    const uint16_t* const Kb = Ks + buf * KBUF;
-    const uint16_t* const Vb = Vs + buf * VBUF;
+    const uint16_t* const Kb = Ks + buf * KBUF + sbo * 32 * kKS;   // (this wave's key half)
+    const uint16_t* const Vb = Vs + buf * VBUF + sbo * 32 * kVS;
     // LEAN: one K and one V fragment set, each re-read right after its last reader (K of
     // sub-block sb+1 after the last Q K^T on sb, V of sb after the last P V on sb-1)
     constexpr bool kLean = (FORM & 1) != 0;
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       for (int r = 0; r < 16; ++r) {
         float s = kF16 ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
         if constexpr (kMasked)
-          if (kt * BK + sb * 32 + acc_row(r, hh) >= K) s = -INFINITY;
+          if (kt * BK + (sbo + sb) * 32 + acc_row(r, hh) >= K) s = -INFINITY;
         e[r] = fast_exp2(s);
       }
 #pragma unroll
@@ -467,10 +477,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       // K of sub-block sb+1: LEAN after this step's Q K^T when it was the last one on sb
       // (b == QB-2: Q K^T of block x+1 = (sb, QB-1)), else early into the other slot
       // (QB == 1: block x+1 is already on sb+1, so its K is read at the start of this step)
-      constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSB;
+      constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSBW;
       constexpr bool kRdKEarly = kLeanK && kRdK && QB == 1;
       // V: LEAN reads V(sb) after this step's P V on block x-1 = (sb-1, QB-1); else V(sb+1) early
-      constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSB);
+      constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSBW);
       // the next tile's chunks go to the other buffer over the second half of the tile (every
       // wave has passed the barrier that ended the tile which last read that buffer)
       // chunks [c0, c1) of this thread are written in this step
@@ -603,7 +613,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     for (int kt = 0; kt < ntiles; ++kt) {
       stage_all(kt, 0, false);
       __syncthreads();
-      for (int sb = 0; sb < NSB; ++sb) {
+      for (int sb = sbo; sb < sbo + NSBW; ++sb) {
         short8_t kf[kNKT];
         short8_t vf[2][kNDT];
         read_k(Ks, sb, kf);
@@ -641,6 +651,37 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       }
       __syncthreads();
     }
+#pragma unroll
+    for (int b = 0; b < QB; ++b) m_ref[b] = m_run[b];   // (the key-split combine's reference)
+  }
+
+  if constexpr (kKSplit) {
+    // ---- key split: the second half's O (row sums included) and reference points through LDS
+    // (the tile buffers are dead), one query block per round; the first half rescales both to
+    // the larger reference and adds
+    float* const xo = reinterpret_cast<float*>(smem) + wq * (kNDT * 16 * 64 + 64);
+    static_assert(WQ * (kNDT * 16 * 64 + 64) * 4 <= (2 * KBUF + 2 * VBUF) * 2, "combine slots fit the tile buffers");
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      if (khalf == 1) {
+#pragma unroll
+        for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xo[(dt * 16 + r) * 64 + lane] = O[b][dt][r];
+        xo[kNDT * 16 * 64 + lane] = m_ref[b];
+      }
+      __syncthreads();
+      if (khalf == 0) {
+        const float m1 = xo[kNDT * 16 * 64 + lane];
+        const float mx = fmaxf(m_ref[b], m1);
+        const float f0 = fast_exp2(m_ref[b] - mx), f1 = fast_exp2(m1 - mx);
+#pragma unroll
+        for (int dt = 0; dt < kNDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) O[b][dt][r] = O[b][dt][r] * f0 + xo[(dt * 16 + r) * 64 + lane] * f1;
+      }
+      __syncthreads();
+    }
   }
 
   stamp(36);
@@ -648,7 +689,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // (64 cache lines) per instruction; the wave writes its rows to LDS instead (the tile buffers
   // are dead: every wave has passed the last tile's barrier) and stores them back as contiguous
   // 16-byte chunks, consecutive lanes along a row
-  uint16_t* const orow = smem + wave * (32 * QB * kOS);
+  if (kKSplit && khalf != 0) return;   // (key split: the first half holds the combined rows)
+  uint16_t* const orow = smem + wq * (32 * QB * kOS);
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const float l = __shfl(O[b][kLdt][kLr], lane & 31);
@@ -685,7 +727,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 template <int D, int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
 hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
-  b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
+  constexpr int WQ = (FORM & 524288) != 0 ? WAVES / 2 : WAVES;   // query waves (key split: half)
+  b.n_qtiles = (a.P + 32 * QB * WQ - 1) / (32 * QB * WQ);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
   hipLaunchKernelGGL((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
@@ -721,6 +764,10 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
       case 102: return (int)launch<80, 8, 1, 128, true, 1>(a, st);
       case 103: return (int)launch<80, 4, 2, 128, true, 1 | 16>(a, st);   // 92 with clock stamps
       case 128: return (int)launch<80, 4, 2, 128, true, 1 | 8192>(a, st);  // default, heads fastest
+      // key split: 8 waves, wave w and w + 4 on the two key halves of each tile (two waves per SIMD)
+      case 143: return (int)launch<80, 8, 2, 128, true, 1 | 524288>(a, st);
+      case 144: return (int)launch<80, 8, 2, 128, true, 1 | 128 | 524288>(a, st);   // + split staging
+      case 145: return (int)launch<80, 8, 1, 128, true, 1 | 524288>(a, st);
 #endif
       default: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
     }
