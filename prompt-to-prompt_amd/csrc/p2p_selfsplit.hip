@@ -18,11 +18,9 @@
 namespace p2p {
 namespace {
 
-// D: head dim (multiple of 32, no padding columns); W waves x KBW 32-key blocks per wave; QB
-// 32-query blocks per workgroup (QB = 2: every K / V fragment feeds two MFMAs, half the
-// workgroups' K / V traffic through the CUs; partials combined one query block per round)
-template <int D, int W, int KBW, int QB = 1>
-__global__ __launch_bounds__(64 * W, QB == 1 ? 2 : 1) void self_split_kernel(SelfArgs a) {
+// D: head dim (multiple of 32, no padding columns); W waves x KBW 32-key blocks per wave
+template <int D, int W, int KBW>
+__global__ __launch_bounds__(64 * W, 2) void self_split_kernel(SelfArgs a) {
   static_assert(D % 32 == 0, "d tiles without padding");
   constexpr int NKT = D / 16;      // 16-deep k steps of Q K^T
   constexpr int NDT = D / 32;      // 32-row tiles of O^T
@@ -31,10 +29,10 @@ __global__ __launch_bounds__(64 * W, QB == 1 ? 2 : 1) void self_split_kernel(Sel
   static_assert(VStrideBf16<D>::value == D, "dense V rows are conflict-free for the transposed reads");
   constexpr int VREG = KW * VROW;  // bytes of one wave's V region
   constexpr int OS = D + 4;          // O partial row stride (floats): rows on distinct banks
-  constexpr int OREG = 32 * OS * 4;  // its O partial of one query block: [32 rows][OS] f32
+  constexpr int OREG = 32 * OS * 4;  // its O partial: [32 rows][OS] f32
   constexpr int REG = VREG > OREG ? VREG : OREG;
   __shared__ __attribute__((aligned(16))) char smem[W * REG];
-  __shared__ float ml[W][QB][2][32];  // m_w, l_w of every row
+  __shared__ float ml[W][2][32];      // m_w, l_w of every row
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -50,6 +48,8 @@ __global__ __launch_bounds__(64 * W, QB == 1 ? 2 : 1) void self_split_kernel(Sel
   const int src = a.qk_src[n];
   const int K = a.K;
   const float c = a.scale_log2;
+  const int p = qt * 32 + qi;
+  const bool prow = p < a.P;
   const int key0 = wave * KW;
 
   const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * D;
@@ -78,14 +78,10 @@ __global__ __launch_bounds__(64 * W, QB == 1 ? 2 : 1) void self_split_kernel(Sel
                                        16, 0, 0);
     }
   }
-  short8_t qf[QB][NKT];
+  short8_t qf[NKT];
 #pragma unroll
-  for (int b = 0; b < QB; ++b) {
-    const int p = (qt * QB + b) * 32 + qi;
-#pragma unroll
-    for (int t = 0; t < NKT; ++t)
-      qf[b][t] = p < a.P ? *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + 16 * t + 8 * hh) : short8_t{};
-  }
+  for (int t = 0; t < NKT; ++t)
+    qf[t] = prow ? *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + 16 * t + 8 * hh) : short8_t{};
   short8_t kf[KBW][NKT];
 #pragma unroll
   for (int kb = 0; kb < KBW; ++kb) {
@@ -94,117 +90,90 @@ __global__ __launch_bounds__(64 * W, QB == 1 ? 2 : 1) void self_split_kernel(Sel
     for (int t = 0; t < NKT; ++t) kf[kb][t] = *reinterpret_cast<const short8_t*>(kp + (int64_t)key * a.ldk + 16 * t + 8 * hh);
   }
 
-  // ---- S^T = K_w Q^T, the wave's row max and exponentials (per query block)
-  float sv[QB][KBW][16];
-  float mx[QB], ls[QB];
+  // ---- S^T = K_w Q^T, the wave's row max and exponentials
+  float sv[KBW][16];
 #pragma unroll
-  for (int b = 0; b < QB; ++b) {
+  for (int kb = 0; kb < KBW; ++kb) {
+    f32x16_t acc = {};
 #pragma unroll
-    for (int kb = 0; kb < KBW; ++kb) {
-      f32x16_t acc = {};
+    for (int t = 0; t < NKT; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf[kb][t]),
+                                                    __builtin_bit_cast(bf16x8_t, qf[t]), acc, 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < NKT; ++t)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf[kb][t]),
-                                                      __builtin_bit_cast(bf16x8_t, qf[b][t]), acc, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        sv[b][kb][r] = (key0 + kb * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
-    }
-    float m = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < KBW; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) m = fmaxf(m, sv[b][kb][r]);
-    m = fmaxf(m, other_half(m)) * c;   // every wave owns >= 1 key below K: m is finite
-    float l = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < KBW; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = fast_exp2(fmaf(sv[b][kb][r], c, -m));
-        sv[b][kb][r] = e;
-        l += e;
-      }
-    mx[b] = m;
-    ls[b] = l + other_half(l);
+    for (int r = 0; r < 16; ++r)
+      sv[kb][r] = (key0 + kb * 32 + acc_row(r, hh) < K) ? acc[r] : -INFINITY;
   }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[kb][r]);
+  mx = fmaxf(mx, other_half(mx)) * c;   // every wave owns >= 1 key below K: mx is finite
+  float ls = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KBW; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = fast_exp2(fmaf(sv[kb][r], c, -mx));
+      sv[kb][r] = e;
+      ls += e;
+    }
+  ls += other_half(ls);
 
-  // ---- O_w^T = V_w^T P^T once the wave's V rows have landed; each V^T fragment feeds QB MFMAs
+  // ---- O_w^T = V_w^T P^T once the wave's V rows have landed
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA (and every other load) retired
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  f32x16_t O[QB][NDT];
+  f32x16_t O[NDT];
 #pragma unroll
-  for (int b = 0; b < QB; ++b)
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) O[b][dt] = f32x16_t{};
-#pragma unroll
-  for (int kb = 0; kb < KBW; ++kb)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      MmaBf16::frag pb[QB];
-#pragma unroll
-      for (int b = 0; b < QB; ++b) pb[b] = MmaBf16::pack_p(sv[b][kb] + 8 * s2);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const MmaBf16::frag va = vt_frag<D>(Vw, kb * 32, s2, dt * 32, lane);
-#pragma unroll
-        for (int b = 0; b < QB; ++b) MmaBf16::mma(O[b][dt], va, pb[b]);
-      }
-    }
-  if (hh == 0)
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      ml[wave][b][0][qi] = mx[b];
-      ml[wave][b][1][qi] = ls[b];
-    }
+  for (int kb = 0; kb < KBW; ++kb) pv_block<D, NDT>(MmaBf16{}, O, Vw, kb * 32, sv[kb], lane);
 
-  // ---- per query block: the partial into the wave's own region (its V is dead once every
-  // lane's reads are in), O_w as [32 rows][OS] f32, one barrier, the workgroup combines
-  //   O = sum_w O_w 2^(m_w - M) / sum_w l_w 2^(m_w - M),  M = max_w m_w
+  // ---- the partial into the wave's own region (its V is dead once every lane's reads are in):
+  // O_w as [32 rows][OS] f32; m_w, l_w per row beside it
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float* const Ow = reinterpret_cast<float*>(reg);
 #pragma unroll
-  for (int b = 0; b < QB; ++b) {
-    if (b == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      __syncthreads();   // every thread done combining the previous block
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4_t*>(Ow + qi * OS + dt * 32 + 8 * g + 4 * hh) =
+          f32x4_t{O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2], O[dt][4 * g + 3]};
+  if (hh == 0) {
+    ml[wave][0][qi] = mx;
+    ml[wave][1][qi] = ls;
+  }
+  __syncthreads();
+
+  // ---- combine: thread t -> (row, 4-column chunk) pairs, whole rows of O out as bf16
+  constexpr int CH = 32 * D / 4;   // 4-column chunks of the 32 x D block
+  for (int i = tid; i < CH; i += 64 * W) {
+    const int row = i / (D / 4);
+    const int col = (i - row * (D / 4)) * 4;
+    float m[W], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      m[w] = ml[w][0][row];
+      M = fmaxf(M, m[w]);
     }
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    float L = 0.f;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4_t*>(Ow + qi * OS + dt * 32 + 8 * g + 4 * hh) =
-            f32x4_t{O[b][dt][4 * g], O[b][dt][4 * g + 1], O[b][dt][4 * g + 2], O[b][dt][4 * g + 3]};
-    __syncthreads();
-    constexpr int CH = 32 * D / 4;   // 4-column chunks of the 32 x D block
-    for (int i = tid; i < CH; i += 64 * W) {
-      const int row = i / (D / 4);
-      const int col = (i - row * (D / 4)) * 4;
-      float m[W], M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        m[w] = ml[w][b][0][row];
-        M = fmaxf(M, m[w]);
-      }
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      float L = 0.f;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const float* ow = reinterpret_cast<const float*>(smem + w * REG);
-        const float f = fast_exp2(m[w] - M);
-        L += ml[w][b][1][row] * f;
-        acc += *reinterpret_cast<const f32x4_t*>(ow + row * OS + col) * f;
-      }
-      const int pr = (qt * QB + b) * 32 + row;
-      if (pr < a.P) {
-        const float inv = 1.f / L;
-        uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)pr * a.ldo + col;
-        store4(op, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
-      }
+    for (int w = 0; w < W; ++w) {
+      const float* ow = reinterpret_cast<const float*>(smem + w * REG);
+      const float f = fast_exp2(m[w] - M);
+      L += ml[w][1][row] * f;
+      acc += *reinterpret_cast<const f32x4_t*>(ow + row * OS + col) * f;
+    }
+    const int pr = qt * 32 + row;
+    if (pr < a.P) {
+      const float inv = 1.f / L;
+      uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)pr * a.ldo + col;
+      store4(op, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
     }
   }
 }
@@ -364,12 +333,12 @@ __global__ __launch_bounds__(64 * W, 1) void self_ring_kernel(SelfArgs a) {
   }
 }
 
-template <int D, int W, int KBW, int QB = 1>
+template <int D, int W, int KBW>
 hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
-  b.n_qtiles = (a.P + 32 * QB - 1) / (32 * QB);
+  b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_split_kernel<D, W, KBW, QB>), grid, block, 0, st, b);
+  hipLaunchKernelGGL((self_split_kernel<D, W, KBW>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -393,8 +362,6 @@ bool self_ring_eligible(const SelfArgs& a, int d) {
 int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
   (void)d;
 #ifdef P2P_EXPERIMENTS
-  // key split with two query blocks per workgroup (K <= 256): 4 waves x 64 keys, 64 queries
-  if (a.variant == 146 && a.K <= 256) return (int)launch_split<160, 4, 2, 2>(a, st);
   if (a.variant == 135) return (int)launch_ring<2>(a, st);
   if (a.variant == 136) return (int)launch_ring<1>(a, st);
 #endif
