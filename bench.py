@@ -36,16 +36,24 @@ HBM_PEAK_GBPS = 8000.0          # spec, MI355X_MICROARCH.md:36 (6.29 TB/s measur
 
 class LaunchTimer:
     """HIP events around the launches of interest, on the launch stream (torch's current stream,
-    which the binding launches on): the dominant kernel (G1/G7 self-attention, FLOP) and the
-    HBM-bound map-store launches (the G2/G6 cross-attention calls that keep their maps, and under
-    --store-self the G2/G6 self calls whose maps kept: fused pass + self_maps_kernel), with their
-    algorithmic bytes."""
+    which the binding launches on):
+    * "dominant": the G1/G7 self-attention (FLOP);
+    * "attn": EVERY attention launch of the path (self and cross, all seven geometries), with its
+      algorithmic FLOP 4 P K C N (K = 77 unpadded for cross), for the aggregate roofline
+      the north star names ("45 % of bf16 peak in the attention kernels"), plus a per-geometry split;
+    * the HBM-bound launches (the G2/G6 cross calls that keep their maps, --store-self's kept self
+      maps, the LocalBlend mask and the latent step) with their algorithmic bytes.
+    Every record also carries the index of the batch (edit group) it ran in, so per-batch
+    averages show clock droop over a long run."""
 
     def __init__(self, n_query=4096):
         self.n_query = n_query
-        self.rec = {}            # name -> list of (start event, end event, work)
-        self._pending = None
+        self.rec = {}            # name -> list of (start event, end event, work, batch)
+        self._pending = None     # (start event, [(name, work), ...])
         self.enabled = False
+        self.batch = 0
+        self.batch_marks = []    # one event at the end of each timed batch
+        self.cross_group_kernel = {}   # geometry name -> True when the group cross kernel ran
 
     @staticmethod
     def _bytes(kind, t, info):
@@ -57,29 +65,32 @@ class LaunchTimer:
         maps = 4.0 * info["stored"] * t.n_heads * t.n_query * t.n_key * (2 if info["accumulate"] else 1)
         return io + maps
 
-    def _name(self, kind, t, info):
+    def _names(self, kind, t, info):
+        flop = 4.0 * t.n_query * t.n_key * t.n_heads * t.head_dim * t.n_batch
+        out = [("attn", flop), (f"attn:{kind}:P{t.n_query}:d{t.head_dim}", flop)]
         if kind == "self" and t.n_query == self.n_query and info["stored"] == 0:
-            return "dominant"
+            out.append(("dominant", flop))
         if t.n_query == 1024 and info["stored"] > 0 and info["accumulate"]:
-            return f"{kind}_store_p1024"
-        return None
+            out.append((f"{kind}_store_p1024", self._bytes(kind, t, info)))
+        return out
 
     def before(self, kind, t, info=None):
+        if not self.enabled:
+            return
         info = info or {"stored": 0, "accumulate": False}
-        name = self._name(kind, t, info) if self.enabled else None
-        if name is not None:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            work = (4.0 * t.n_query * t.n_key * t.n_heads * t.head_dim * t.n_batch if name == "dominant"
-                    else self._bytes(kind, t, info))
-            self._pending = (name, ev, work)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self._pending = (ev, self._names(kind, t, info))
+        if kind == "cross" and "n_groups" in info:
+            self.cross_group_kernel[f"attn:cross:P{t.n_query}:d{t.head_dim}"] = bool(info.get("group_kernel"))
 
     def after(self, kind, t, info=None):
         if self._pending is not None:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            name, start, work = self._pending
-            self.rec.setdefault(name, []).append((start, ev, work))
+            start, names = self._pending
+            for name, work in names:
+                self.rec.setdefault(name, []).append((start, ev, work, self.batch))
             self._pending = None
 
     def before_aux(self, name, nbytes):
@@ -87,37 +98,88 @@ class LaunchTimer:
         if self.enabled:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self._pending = (name, ev, float(nbytes))
+            self._pending = (ev, [(name, float(nbytes))])
 
     def after_aux(self, name):
         self.after(name, None)
 
-    def summary(self, name="dominant"):
+    def end_batch(self):
+        if self.enabled:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.batch_marks.append(ev)
+            self.batch += 1
+
+    def summary(self, name="dominant", batch=None):
         """(average ms per launch, average work per launch, launches)"""
         torch.cuda.synchronize()
-        pairs = self.rec.get(name, [])
+        pairs = [r for r in self.rec.get(name, []) if batch is None or r[3] == batch]
         if not pairs:
             return None, None, 0
-        ms = [a.elapsed_time(b) for a, b, _ in pairs]
-        return sum(ms) / len(ms), sum(w for _, _, w in pairs) / len(pairs), len(ms)
+        ms = [a.elapsed_time(b) for a, b, _, _ in pairs]
+        return sum(ms) / len(ms), sum(w for _, _, w, _ in pairs) / len(pairs), len(ms)
+
+    def attn_total(self, peak, unet_calls):
+        """Aggregate roofline of ALL attention launches: summed algorithmic FLOP / summed HIP-event
+        time, and the per-geometry split (average launch, its FLOP and fraction of peak)."""
+        torch.cuda.synchronize()
+        recs = self.rec.get("attn", [])
+        if not recs:
+            return None
+        tot_ms = sum(a.elapsed_time(b) for a, b, _, _ in recs)
+        tot_flop = sum(w for _, _, w, _ in recs)
+        achieved = tot_flop / (tot_ms * 1e-3) / 1e12
+        by = []
+        for name in sorted(k for k in self.rec if k.startswith("attn:")):
+            avg_ms, flop, n = self.summary(name)
+            tf = flop / (avg_ms * 1e-3) / 1e12
+            d = {"geometry": name[5:], "launches": n, "avg_launch_ms": avg_ms, "flop_per_launch": flop,
+                 "achieved_tflops": tf, "frac": tf / peak, "share_of_attn_time": avg_ms * n / tot_ms}
+            if name in self.cross_group_kernel:
+                d["kernel"] = "cross_group_kernel" if self.cross_group_kernel[name] else "cross_attn_kernel"
+            by.append(d)
+        return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                "launches": len(recs), "attn_ms_total": tot_ms,
+                "attn_ms_per_unet_call": tot_ms / unet_calls if unet_calls else None,
+                "flop_per_unet_call": tot_flop / unet_calls if unet_calls else None,
+                "rule": "sum over every self/cross attention launch of the timed run of 4 P K C N FLOP "
+                        "(K = 77 unpadded for cross; SURVEY §8d) / sum of their HIP-event launch times",
+                "by_geometry": by}
+
+    def per_batch(self):
+        """Per-batch GPU ms (event to event) and the dominant kernel's average launch per batch."""
+        torch.cuda.synchronize()
+        out = []
+        for i in range(1, len(self.batch_marks)):
+            dom, _, _ = self.summary("dominant", batch=i)
+            out.append((i, self.batch_marks[i - 1].elapsed_time(self.batch_marks[i]), dom))
+        return out
 
     def hbm_lines(self):
         out = []
-        labels = {"cross_store_p1024": "cross_attn_kernel G2/G6 (P=1024, d=80, K=77) with the kept cross maps "
-                                       "(read-add-write) + LocalBlend word sums",
+        labels = {"cross_store_p1024": "cross-attention G2/G6 (P=1024, d=80, K=77) with the kept cross maps "
+                                       "(read-add-write)",
                   "self_store_p1024": "self-attention G2/G6 (P=K=1024, d=80) with the kept self maps: fused "
                                       "pass (lse) + self_maps_kernel read-add-write",
                   "localblend": "LocalBlend mask (blend_finalize_kernel: folded word sums -> pooled, thresholded "
                                 "64x64 mask)",
-                  "latent_step": "latent_step_kernel (CFG + DDIM + LocalBlend blend)"}
+                  "latent_step": "latent_step_kernel (CFG + DDIM + LocalBlend blend with a precomputed mask)",
+                  "latent_blend": "latent_blend_kernel: LocalBlend in one launch with the latent update (folded word "
+                                  "sums -> mean, 3x3 max-pool, upsample, normalise, threshold -> blend) + CFG + DDIM"}
         rules = {"localblend": "word sums read (B x 2 x L*H x 16^2 f32) + mask written (B x 64^2 u8)",
-                 "latent_step": "eps read (2B x 4 x 64^2, bf16) + latents read and written (f32) + mask read"}
-        for name in ("cross_store_p1024", "self_store_p1024", "localblend", "latent_step"):
+                 "latent_step": "eps read (2B x 4 x 64^2, bf16) + latents read and written (f32) + mask read",
+                 "latent_blend": "eps read (2B x 4 x 64^2, bf16) + latents read and written (f32) + folded word sums "
+                                 "read once (B x 2 x L*H x 16^2 f32)"}
+        for name in ("cross_store_p1024", "self_store_p1024", "localblend", "latent_step", "latent_blend"):
             avg_ms, nbytes, n = self.summary(name)
             if not n:
                 continue
             gbps = nbytes / (avg_ms * 1e-3) / 1e9
-            out.append({"kernel": labels[name], "avg_launch_ms": avg_ms, "launches": n,
+            label = labels[name]
+            if name == "cross_store_p1024":
+                label = (("cross_group_kernel" if self.cross_group_kernel.get("attn:cross:P1024:d80") else
+                          "cross_attn_kernel") + " " + label)
+            out.append({"kernel": label, "avg_launch_ms": avg_ms, "launches": n,
                         "algorithmic_bytes": nbytes, "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": gbps / HBM_PEAK_GBPS,
                         "bytes_rule": rules.get(name, "q + o + k + v (io dtype) + kept maps f32 x2 (read + write, "
@@ -259,9 +321,13 @@ def main():
     timer.enabled = True
     t0 = time.perf_counter()
 
-    def progress(i, n):   # long sweeps: a progress line per batch (stderr; host-side only)
+    timer.end_batch()     # (batch 0's start mark)
+
+    def progress(i, n):   # a progress line per batch (stderr; host-side only) + the batch's end event
+        timer.end_batch()
         if n > 4:
-            print(f"[bench rank {rank}] batch {i + 1}/{n}", file=sys.stderr, flush=True)
+            print(f"[bench rank {rank}] batch {i + 1}/{n} host {1e3 * (time.perf_counter() - t0):.0f} ms",
+                  file=sys.stderr, flush=True)
 
     # the sweep tests/test_distributed.py runs over gloo: this rank's batches, then ONE RCCL
     # all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
@@ -283,8 +349,15 @@ def main():
     assert (maps_all[:, 0].sum(-1) - 1).abs().max().item() < 1e-2
 
     avg_ms, flops, n_launch = timer.summary()
+    peak = MFMA_PEAK_BF16_TFLOPS if args.compute == "bf16" else MFMA_PEAK_F32_TFLOPS
+    # per-batch GPU time and the dominant kernel's average launch in that batch (stderr): clock
+    # droop over a long run shows up here, not in the one-line average
+    for i, ms_b, dom in timer.per_batch():
+        print(f"[bench rank {rank}] batch {i} gpu {ms_b:.1f} ms  dominant avg "
+              f"{dom * 1e3 if dom else float('nan'):.1f} us", file=sys.stderr, flush=True)
+    unet_calls = len(sweep.batches(all_seeds, rank, world, G)) * args.ddim_steps   # this rank's U-Net calls
+    attn_total = timer.attn_total(peak, unet_calls)
     if rank == 0:
-        peak = MFMA_PEAK_BF16_TFLOPS if args.compute == "bf16" else MFMA_PEAK_F32_TFLOPS
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms else None
         traffic, traffic_src = pmc_traffic() if G == 1 else (None, "no PMC pass at N = 8G")
         roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -313,6 +386,9 @@ def main():
                        "self_maps_kept": args.store_self, "gathered": "final latents + 16x16 cross maps (1 all-gather)",
                        "parallelism": f"replicas x{world} (groups by seed)"},
             "roofline": roofline, "cpu_baseline": cpu,
+            # every attention launch of the timed run together (north star: ">= 45 % of bf16 MFMA peak
+            # in the attention kernels"), HIP-event timed, with the per-geometry split
+            "roofline_attn_total": attn_total,
             # the HBM-bound launches of the path (north star: "achieved HBM GB/s for the map and blend
             # kernels"), HIP-event timed in the same run; algorithmic bytes, not PMC
             "roofline_hbm": timer.hbm_lines(),

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 12
+#define P2P_ABI_VERSION 13
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -215,6 +215,19 @@ typedef struct {
   const uint8_t* mask;
   int32_t group_size;              /* prompts per prompt group (0 = one group of n_prompts) */
   const uint8_t* group_blend;      /* [n_prompts / group_size] 1 = blend this group, NULL = all */
+  /* LocalBlend in the same launch (one kernel per denoising step): when blend_sums[g] is set,
+   * prompt group g's mask is built here from the running word sums the cross-attention store
+   * epilogue folded (p2p_group.blend_sums: [group_size, 2, blend_lh, blend_res^2] f32) --
+   * mean over the blend_lh layer x head maps, 3x3 max-pool, nearest upsampling, per-image max
+   * normalisation, thresholds, mask[:1] | mask and the substruct gate (null_text.py:41-67),
+   * exactly as p2p_localblend with word_sums_ready = 1 builds it -- and the blend of
+   * null_text.py:68-70 follows.  `mask` must then be NULL; NULL entries do not blend.
+   * (ptp_utils.py:75 step_callback + null_text.py:41-70, fused with the CFG/DDIM update.) */
+  const float* blend_sums[P2P_MAX_GROUPS];
+  int32_t blend_lh;                /* layer x head maps per prompt (5 x 8)                   */
+  int32_t blend_res;               /* map resolution (16); res^2 <= 256, <= lat_h, lat_w     */
+  float blend_th_pool, blend_th_sub;
+  int32_t blend_sub;               /* 1: the substruct sums (index 1) gate the mask          */
 } p2p_latent_step_args;
 
 int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream);

@@ -78,25 +78,38 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
-  const int b = blockIdx.x;
-  const int R = a.map_res;
-  const int R2 = R * R;
-  const int LH = a.n_maps * a.heads_per_map;
-  const int HW = a.lat_h * a.lat_w;
-  __shared__ float mean_a[2][256];   // [0] = source prompt, [1] = prompt b
-  __shared__ float mean_s[2][256];
-  __shared__ float pooled[2][256];
-  __shared__ float red[4][4];        // per-wave maxima: (pooled, substruct) x (source, b)
-  const int tid = threadIdx.x;
-  const bool sub = a.substruct_layers != nullptr;
+// LDS of one mask build (256 threads): mean maps, pooled maps, per-wave maxima, the mask per map
+// pixel.  [0] = the group's source prompt, [1] = prompt b
+struct BlendLds {
+  float mean_a[2][256];
+  float mean_s[2][256];
+  float pooled[2][256];
+  float red[4][4];
+  float msrc[256];
+};
 
+// nearest upsampling (F.interpolate default): latent pixel yx -> map pixel
+__device__ __forceinline__ int blend_src_of(int yx, int R, int lat_h, int lat_w) {
+  const float sy = (float)R / (float)lat_h, sx = (float)R / (float)lat_w;
+  const int Y = yx / lat_w, X = yx - Y * lat_w;
+  return min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
+}
+
+// Prompt b's LocalBlend mask per map pixel (L.msrc, 1.f / 0.f) from the word sums of its group's
+// source prompt (ws0) and its own (wsb), each [2, LH, R*R] (index 0: alpha-weighted, 1:
+// substruct-weighted): mean over the LH maps, 3x3 max-pool, per-image max of the upsampled map,
+// thresholds, mask[:1] | mask, substruct gate (null_text.py:41-67).  Called by all 256 threads of
+// the workgroup (it synchronises); blend_finalize_kernel and latent_blend_kernel share it, so
+// both build the same mask bit for bit.
+__device__ void build_blend_mask(const float* ws0, const float* wsb, int LH, int R, int lat_h, int lat_w,
+                                 float th_pool, float th_sub, bool sub, BlendLds& L) {
+  const int R2 = R * R;
+  const int tid = threadIdx.x;
   // mean over the L*H maps (sum in index order, then / L*H as Tensor.mean does)
-  for (int i = tid; i < 2 * R2; i += blockDim.x) {
+  for (int i = tid; i < 2 * R2; i += 256) {
     const int k = i / R2, pix = i - k * R2;
-    const int bb = k ? b : 0;
-    const float* wa = a.word_sums + (int64_t)(bb * 2 + 0) * LH * R2 + pix;
-    const float* ws = a.word_sums + (int64_t)(bb * 2 + 1) * LH * R2 + pix;
+    const float* wa = (k ? wsb : ws0) + pix;
+    const float* ws = (k ? wsb : ws0) + (int64_t)LH * R2 + pix;
     float sa = 0.f, ss = 0.f;
     // every load in flight at once (the five blended 16x16 layers x 8 heads = 40 maps: one memory
     // round trip instead of three), then the in-order sums
@@ -107,7 +120,7 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
       for (int u = 0; u < kBatch; ++u) {
         const int j = min(j0 + u, LH - 1);
         va[u] = wa[(int64_t)j * R2];
-        vs[u] = ws[(int64_t)j * R2];
+        vs[u] = sub ? ws[(int64_t)j * R2] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < kBatch; ++u)
@@ -116,69 +129,74 @@ __global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
           ss += vs[u];
         }
     }
-    mean_a[k][pix] = sa / (float)LH;
-    mean_s[k][pix] = ss / (float)LH;
+    L.mean_a[k][pix] = sa / (float)LH;
+    L.mean_s[k][pix] = ss / (float)LH;
   }
   __syncthreads();
   // 3x3 max-pool, stride 1, padding 1 (padding never wins: -inf)
-  for (int i = tid; i < 2 * R2; i += blockDim.x) {
+  for (int i = tid; i < 2 * R2; i += 256) {
     const int k = i / R2, pix = i - k * R2;
     const int y = pix / R, x = pix - y * R;
     float m = -INFINITY;
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
         const int yy = y + dy, xx = x + dx;
-        if (yy >= 0 && yy < R && xx >= 0 && xx < R) m = fmaxf(m, mean_a[k][yy * R + xx]);
+        if (yy >= 0 && yy < R && xx >= 0 && xx < R) m = fmaxf(m, L.mean_a[k][yy * R + xx]);
       }
-    pooled[k][pix] = m;
+    L.pooled[k][pix] = m;
   }
   __syncthreads();
   // per-image max of the nearest-upsampled maps.  Upsampling (latent >= map resolution) samples
   // every source pixel, so the max over the grid is the max over the R*R sources.
-  const float sy = (float)R / (float)a.lat_h, sx = (float)R / (float)a.lat_w;
-  auto src_of = [&](int yx) {
-    const int Y = yx / a.lat_w, X = yx - Y * a.lat_w;
-    return min((int)floorf(Y * sy), R - 1) * R + min((int)floorf(X * sx), R - 1);
-  };
-  const bool all_sources = a.lat_h >= R && a.lat_w >= R;
+  const bool all_sources = lat_h >= R && lat_w >= R;
   float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int i = tid; i < (all_sources ? R2 : HW); i += blockDim.x) {
-    const int src = all_sources ? i : src_of(i);
-    m[0] = fmaxf(m[0], pooled[0][src]);
-    m[1] = fmaxf(m[1], mean_s[0][src]);
-    m[2] = fmaxf(m[2], pooled[1][src]);
-    m[3] = fmaxf(m[3], mean_s[1][src]);
+  for (int i = tid; i < (all_sources ? R2 : lat_h * lat_w); i += 256) {
+    const int src = all_sources ? i : blend_src_of(i, R, lat_h, lat_w);
+    m[0] = fmaxf(m[0], L.pooled[0][src]);
+    m[1] = fmaxf(m[1], L.mean_s[0][src]);
+    m[2] = fmaxf(m[2], L.pooled[1][src]);
+    m[3] = fmaxf(m[3], L.mean_s[1][src]);
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) m[c] = wave_max(m[c]);
   if ((tid & 63) == 0)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) red[tid >> 6][c] = m[c];
+    for (int c = 0; c < 4; ++c) L.red[tid >> 6][c] = m[c];
   __syncthreads();
   float vmax[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    vmax[c] = red[0][c];
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) vmax[c] = fmaxf(vmax[c], red[w][c]);
+    vmax[c] = L.red[0][c];
+    for (int w = 1; w < 4; ++w) vmax[c] = fmaxf(vmax[c], L.red[w][c]);
   }
   // mask of prompt b per source pixel (the thresholds of null_text.py:62-67), then gathered by
-  // the nearest upsampling: identical per output pixel, evaluated 256 times instead of H*W
-  __shared__ float msrc[256];
-  for (int pix = tid; pix < R2; pix += blockDim.x) {
-    const bool m0 = pooled[0][pix] / vmax[0] > a.th_pool;
-    const bool mb = pooled[1][pix] / vmax[2] > a.th_pool;
+  // the nearest upsampling: identical per output pixel, evaluated R*R times instead of H*W
+  for (int pix = tid; pix < R2; pix += 256) {
+    const bool m0 = L.pooled[0][pix] / vmax[0] > th_pool;
+    const bool mb = L.pooled[1][pix] / vmax[2] > th_pool;
     bool mask = m0 || mb;
     if (sub) {
-      const bool s0 = mean_s[0][pix] / vmax[1] > a.th_sub;
-      const bool sb = mean_s[1][pix] / vmax[3] > a.th_sub;
+      const bool s0 = L.mean_s[0][pix] / vmax[1] > th_sub;
+      const bool sb = L.mean_s[1][pix] / vmax[3] > th_sub;
       mask = mask && !(s0 || sb);
     }
-    msrc[pix] = mask ? 1.f : 0.f;
+    L.msrc[pix] = mask ? 1.f : 0.f;
   }
   __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
+  const int b = blockIdx.x;
+  const int R = a.map_res;
+  const int R2 = R * R;
+  const int LH = a.n_maps * a.heads_per_map;
+  const int HW = a.lat_h * a.lat_w;
+  __shared__ BlendLds L;
+  build_blend_mask(a.word_sums, a.word_sums + (int64_t)b * 2 * LH * R2, LH, R, a.lat_h, a.lat_w, a.th_pool,
+                   a.th_sub, a.substruct_layers != nullptr, L);
   // x_t[b] = x_t[0] + mask * (x_t[b] - x_t[0])
-  for (int yx = tid; yx < HW; yx += blockDim.x) {
-    const float mf = msrc[src_of(yx)];
+  for (int yx = threadIdx.x; yx < HW; yx += blockDim.x) {
+    const float mf = L.msrc[blend_src_of(yx, R, a.lat_h, a.lat_w)];
     if (a.mask_out) a.mask_out[(int64_t)b * HW + yx] = mf != 0.f ? 1 : 0;
     if (b == 0 || !a.x_t) continue;  // x_t[0] + mask * 0 == x_t[0]; mask-only mode
     for (int ch = 0; ch < a.channels; ++ch) {
@@ -216,16 +234,45 @@ __device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, 
 __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float sub_rn(float a, float b) { return __fsub_rn(a, b); }
 
+// prev_sample from one element's inputs (CFG combine + DDIM step): eu / ec the unconditional and
+// conditional eps (ec unused without CFG), x the latent
+template <bool BF16>
+__device__ __forceinline__ float ddim_from(const p2p_latent_step_args& a, float eu, float ec, float x) {
+  auto rd = [](float v) { return BF16 ? rnd_bf16(v) : v; };
+  float noise;
+  if (a.cfg) {
+    const float diff = rd(sub_rn(ec, eu));
+    const float gd = rd(mul_rn(a.guidance, diff));
+    noise = rd(add_rn(eu, gd));
+  } else {
+    noise = eu;
+  }
+  // a 0-dim f32 factor times a bf16 tensor: torch casts the factor to bf16 first
+  const float t1 = rd(mul_rn(rd(a.sqrt_beta_t), noise));
+  const float x0 = __fdiv_rn(sub_rn(x, t1), a.sqrt_alpha_t);
+  const float dir = rd(mul_rn(rd(a.sqrt_one_minus_alpha_prev), noise));
+  return add_rn(mul_rn(a.sqrt_alpha_prev, x0), dir);
+}
+
+template <bool BF16>
+__device__ __forceinline__ float eps_at(const p2p_latent_step_args& a, int64_t idx) {
+  if constexpr (BF16) return bf2f(static_cast<const uint16_t*>(a.eps)[idx]);
+  else return static_cast<const float*>(a.eps)[idx];
+}
+
+// prev_sample of prompt b at element i of its [C, H, W] latent
+template <bool BF16>
+__device__ __forceinline__ float ddim_prev(const p2p_latent_step_args& a, int b, int64_t i, int64_t chw) {
+  const float eu = eps_at<BF16>(a, (int64_t)b * chw + i);
+  const float ec = a.cfg ? eps_at<BF16>(a, (int64_t)(a.n_prompts + b) * chw + i) : 0.f;
+  return ddim_from<BF16>(a, eu, ec, a.x[(int64_t)b * chw + i]);
+}
+
 template <bool BF16>
 __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a, int64_t chw) {
   const int HW = a.height * a.width;
   const int B = a.n_prompts;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  auto rd = [](float x) { return BF16 ? rnd_bf16(x) : x; };
-  auto ld = [&](int64_t idx) {
-    if constexpr (BF16) return bf2f(static_cast<const uint16_t*>(a.eps)[idx]);
-    else return static_cast<const float*>(a.eps)[idx];
-  };
   const int gs = a.group_size > 0 ? a.group_size : B;   // prompts per prompt group
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < chw; i += stride) {
     const int yx = (int)(i % HW);
@@ -233,22 +280,7 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
     bool blend = false;
     for (int b = 0; b < B; ++b) {
       const int bg = b % gs;                              // position inside its group
-      float noise;
-      if (a.cfg) {
-        const float eu = ld((int64_t)b * chw + i);
-        const float ec = ld((int64_t)(B + b) * chw + i);
-        const float diff = rd(sub_rn(ec, eu));
-        const float gd = rd(mul_rn(a.guidance, diff));
-        noise = rd(add_rn(eu, gd));
-      } else {
-        noise = ld((int64_t)b * chw + i);
-      }
-      const float x = a.x[(int64_t)b * chw + i];
-      // a 0-dim f32 factor times a bf16 tensor: torch casts the factor to bf16 first
-      const float t1 = rd(mul_rn(rd(a.sqrt_beta_t), noise));
-      const float x0 = __fdiv_rn(sub_rn(x, t1), a.sqrt_alpha_t);
-      const float dir = rd(mul_rn(rd(a.sqrt_one_minus_alpha_prev), noise));
-      float prev = add_rn(mul_rn(a.sqrt_alpha_prev, x0), dir);
+      float prev = ddim_prev<BF16>(a, b, i, chw);
       if (bg == 0) {
         prev0 = prev;                                     // the group's source prompt
         blend = a.mask && (!a.group_blend || a.group_blend[b / gs]);
@@ -261,12 +293,93 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
   }
 }
 
+// The latent step with LocalBlend's mask built in the same launch (a.blend_sums): grid
+// (pixel chunks, prompts).  A workgroup of an edit prompt b whose group blends builds b's mask
+// per map pixel from the folded word sums (build_blend_mask: ~160 KB of L2-resident sums) and
+// updates its chunk of b's latent -- recomputing the group source's prev_sample, which it blends
+// towards, from the same inputs (bit-identical to the source workgroup's).  No workgroup reads
+// another's output.  The kernel is latency-bound (1 MB per step): every thread issues all its
+// eps / x loads (kPxT pixels x up to 4 channels, for b and the source) before the mask build's
+// loads, so the whole launch waits about two memory round trips.
+template <bool BF16>
+__global__ __launch_bounds__(256) void latent_blend_kernel(p2p_latent_step_args a, int64_t chw, int px_per_wg) {
+  constexpr int kPxT = 4;     // latent pixels per thread
+  constexpr int kCg = 4;      // channels per pass (SD latents: 4)
+  const int HW = a.height * a.width;
+  const int b = blockIdx.y;
+  const int gs = a.group_size > 0 ? a.group_size : a.n_prompts;
+  const int g = b / gs, bg = b - g * gs, b0 = b - bg;
+  const float* ws = a.blend_sums[g];
+  const bool blend = bg != 0 && ws != nullptr;          // workgroup-uniform
+  __shared__ BlendLds L;
+  const int px = blockIdx.x * px_per_wg + threadIdx.x * kPxT;
+  for (int c0 = 0; c0 < a.channels; c0 += kCg) {
+    float eu[2][kCg][kPxT], ec[2][kCg][kPxT], xv[2][kCg][kPxT];
+    // every load of this pass first (the source's only when blending)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int bb = s2 ? b0 : b;
+#pragma unroll
+      for (int c = 0; c < kCg; ++c)
+#pragma unroll
+        for (int j = 0; j < kPxT; ++j) {
+          const bool live = (s2 == 0 || blend) && c0 + c < a.channels && px + j < HW;
+          const int64_t i = (int64_t)(c0 + c) * HW + px + j;
+          eu[s2][c][j] = live ? eps_at<BF16>(a, (int64_t)bb * chw + i) : 0.f;
+          ec[s2][c][j] = live && a.cfg ? eps_at<BF16>(a, (int64_t)(a.n_prompts + bb) * chw + i) : 0.f;
+          xv[s2][c][j] = live ? a.x[(int64_t)bb * chw + i] : 0.f;
+        }
+    }
+    if (blend && c0 == 0) {
+      const int R2 = a.blend_res * a.blend_res;
+      build_blend_mask(ws, ws + (int64_t)bg * 2 * a.blend_lh * R2, a.blend_lh, a.blend_res, a.height, a.width,
+                       a.blend_th_pool, a.blend_th_sub, a.blend_sub != 0, L);
+    }
+#pragma unroll
+    for (int c = 0; c < kCg; ++c)
+#pragma unroll
+      for (int j = 0; j < kPxT; ++j) {
+        if (c0 + c >= a.channels || px + j >= HW) continue;
+        float prev = ddim_from<BF16>(a, eu[0][c][j], ec[0][c][j], xv[0][c][j]);
+        if (blend) {
+          const float prev0 = ddim_from<BF16>(a, eu[1][c][j], ec[1][c][j], xv[1][c][j]);
+          const float m = L.msrc[blend_src_of(px + j, a.blend_res, a.height, a.width)];
+          prev = add_rn(prev0, mul_rn(m, sub_rn(prev, prev0)));
+        }
+        a.out[(int64_t)b * chw + (int64_t)(c0 + c) * HW + px + j] = prev;
+      }
+  }
+}
+
 int run_latent_step(const p2p_latent_step_args& a, hipStream_t st) {
   if (!a.eps || !a.x || !a.out || a.n_prompts < 1 || a.channels < 1 || a.height < 1 || a.width < 1 ||
       a.group_size < 0 || (a.group_size > 0 && a.n_prompts % a.group_size))
     return P2P_E_ARG;
   if (a.eps_dtype != P2P_DTYPE_F32 && a.eps_dtype != P2P_DTYPE_BF16) return P2P_E_DTYPE;
   const int64_t chw = (int64_t)a.channels * a.height * a.width;
+  const int gs = a.group_size > 0 ? a.group_size : a.n_prompts;
+  const int n_groups = a.n_prompts / gs;
+  bool fused = false;
+  for (int g = 0; g < P2P_MAX_GROUPS; ++g) {
+    if (!a.blend_sums[g]) continue;
+    if (g >= n_groups) return P2P_E_ARG;
+    fused = true;
+  }
+  if (fused) {
+    // the mask comes from the word sums; a precomputed mask as well would be ambiguous.  out must
+    // not alias x: a source workgroup's writes would race with the edit workgroups' reads of x[g0]
+    if (a.mask || a.group_blend || a.out == a.x || a.blend_lh < 1 || a.blend_res < 1 ||
+        a.blend_res * a.blend_res > 256 || a.blend_res > a.height || a.blend_res > a.width)
+      return P2P_E_ARG;
+    constexpr int kPx = 1024;   // latent pixels per workgroup: 256 threads x 4
+    const int hw = a.height * a.width;
+    dim3 grid((hw + kPx - 1) / kPx, a.n_prompts);
+    if (a.eps_dtype == P2P_DTYPE_BF16)
+      hipLaunchKernelGGL(latent_blend_kernel<true>, grid, dim3(256), 0, st, a, chw, kPx);
+    else
+      hipLaunchKernelGGL(latent_blend_kernel<false>, grid, dim3(256), 0, st, a, chw, kPx);
+    return (int)hipGetLastError();
+  }
   int64_t blocks = (chw + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (a.eps_dtype == P2P_DTYPE_BF16)

@@ -32,7 +32,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class HipError(RuntimeError):
@@ -80,6 +80,8 @@ class LatentArgs(ctypes.Structure):
         ("width", ctypes.c_int32), ("sqrt_beta_t", ctypes.c_float), ("sqrt_alpha_t", ctypes.c_float),
         ("sqrt_alpha_prev", ctypes.c_float), ("sqrt_one_minus_alpha_prev", ctypes.c_float),
         ("mask", ctypes.c_void_p), ("group_size", ctypes.c_int32), ("group_blend", ctypes.c_void_p),
+        ("blend_sums", ctypes.c_void_p * MAX_GROUPS), ("blend_lh", ctypes.c_int32), ("blend_res", ctypes.c_int32),
+        ("blend_th_pool", ctypes.c_float), ("blend_th_sub", ctypes.c_float), ("blend_sub", ctypes.c_int32),
     ]
 
 
@@ -232,6 +234,22 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
     _check(rc, "p2p_self_attn_fwd")
 
 
+def cross_group_dispatch(t: AttnTensors, groups) -> bool:
+    """Whether p2p_cross_attn_fwd runs cross_group_kernel for these arguments: the rule of
+    run_cross / cross_group_eligible (p2p_attn.hip, p2p_cross.hip) -- bf16 inputs and compute, no
+    term-plane program, K <= 96, d in {40, 80, 160}, and >= 512 workgroups (groups x heads x
+    128-row query tiles).  Labels only (bench.py); the library decides."""
+    if t.io_dtype != P2P_DTYPE_BF16 or t.compute != P2P_COMPUTE_BF16 or t.n_key > MAX_KEYS_CROSS:
+        return False
+    if t.head_dim not in (40, 80, 160):
+        return False
+    for grp in groups:
+        prog, count = grp[2], int(grp[1])
+        if prog is not None and count > 1 and not (int(getattr(prog, "p2p_flags", 0)) & 1):
+            return False
+    return len(groups) * t.n_heads * ((t.n_query + 127) // 128) >= 512
+
+
 def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, store_slot=None,
                accumulate=False):
     """groups: list of (first, count, program_tensor|None, alpha_tensor|None[, blend]) with blend =
@@ -263,7 +281,8 @@ def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, sto
     obs = LAUNCH_OBSERVER
     if obs is not None:
         info = {"stored": sum(1 for x in store_slot if int(x) >= 0) if (store is not None and store_slot is not None)
-                else 0, "accumulate": bool(accumulate)}
+                else 0, "accumulate": bool(accumulate), "n_groups": len(groups),
+                "group_kernel": cross_group_dispatch(t, groups)}
         obs.before("cross", t, info)
     rc = lib().p2p_cross_attn_fwd(ctypes.byref(t), G, len(groups),
                                   store.data_ptr() if store is not None else None, slots,
@@ -342,12 +361,15 @@ def store_scale(src: torch.Tensor, divisor: float, out: Optional[torch.Tensor] =
     return out
 
 
-def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, group_blend=None):
+def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, group_blend=None, blend=None):
     """Fused CFG + DDIM step + LocalBlend blend (p2p_latent_step).  eps: [2B or B, C, H, W]
     (f32/bf16, uncond block first when guidance is given); x, out: f32 [B, C, H, W] (out may be
-    x); coeffs: (sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev) floats;
-    mask: uint8 [B, H, W] or None; group_size: prompts per prompt group (0 = one group), with
-    group_blend (uint8 [B / group_size] or None = every group) selecting the groups that blend."""
+    x unless ``blend`` is given); coeffs: (sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev,
+    sqrt_one_minus_alpha_prev) floats; mask: uint8 [B, H, W] or None; group_size: prompts per
+    prompt group (0 = one group), with group_blend (uint8 [B / group_size] or None = every group)
+    selecting the groups that blend.  blend: instead of ``mask``, one entry per prompt group --
+    None (no blend) or (sums f32 [group prompts, 2, lh, res^2], th_pool, th_sub, use_substruct):
+    the folded LocalBlend word sums the mask is built from in the same launch."""
     _require_cuda(eps, x, out, mask)
     for t in (eps, x, out):
         assert t.is_contiguous()
@@ -373,14 +395,37 @@ def latent_step(eps, x, out, coeffs, guidance=None, mask=None, group_size=0, gro
         a.group_blend = group_blend.data_ptr()
     else:
         a.group_blend = None
+    sums_bytes = 0
+    if blend is not None and any(e is not None for e in blend):
+        if mask is not None or group_blend is not None or out.data_ptr() == x.data_ptr():
+            raise HipError("latent_step: blend (folded sums) excludes mask / group_blend and out aliasing x")
+        gs = group_size if group_size > 0 else B
+        if len(blend) != B // gs or len(blend) > MAX_GROUPS:
+            raise HipError(f"latent_step: {len(blend)} blend entries for {B // gs} prompt groups")
+        ref = next(e for e in blend if e is not None)
+        _, th_pool, th_sub, use_sub = ref
+        lh, r2 = ref[0].shape[2], ref[0].shape[3]
+        for g, e in enumerate(blend):
+            if e is None:
+                continue
+            sums = e[0]
+            _require_cuda(sums)
+            if (sums.dtype != torch.float32 or not sums.is_contiguous() or tuple(sums.shape) != (gs, 2, lh, r2)
+                    or tuple(e[1:]) != (th_pool, th_sub, use_sub)):
+                raise HipError("latent_step: blend sums must be f32 [group, 2, lh, res^2] with one threshold set")
+            a.blend_sums[g] = sums.data_ptr()
+            sums_bytes += sums.numel() * 4
+        a.blend_lh, a.blend_res = int(lh), int(round(r2 ** 0.5))
+        a.blend_th_pool, a.blend_th_sub, a.blend_sub = float(th_pool), float(th_sub), int(bool(use_sub))
     obs = LAUNCH_OBSERVER
     if obs is not None and hasattr(obs, "before_aux"):
-        # algorithmic bytes: eps read, x read, out written, mask read
-        obs.before_aux("latent_step", eps.numel() * eps.element_size() + 2 * x.numel() * 4 +
-                       (mask.numel() if mask is not None else 0))
+        # algorithmic bytes: eps read, x read, out written, mask (or the folded word sums) read
+        obs.before_aux("latent_blend" if sums_bytes else "latent_step",
+                       eps.numel() * eps.element_size() + 2 * x.numel() * 4 +
+                       (mask.numel() if mask is not None else 0) + sums_bytes)
     rc = lib().p2p_latent_step(ctypes.byref(a), _stream(x.device))
     if obs is not None and hasattr(obs, "after_aux"):
-        obs.after_aux("latent_step")
+        obs.after_aux("latent_blend" if sums_bytes else "latent_step")
     _check(rc, "p2p_latent_step")
     return out
 

@@ -80,22 +80,49 @@ def fused_local_blend(x_t, attention_store, alpha_flat, sub_flat, th_pool, th_su
     return out.to(x_t.dtype)
 
 
+class FoldedBlendMask:
+    """One prompt group's LocalBlend mask in the form it is built from: the running word sums
+    [B, 2, lh, res^2] that the cross-attention store epilogue folded (AttentionControlEdit.
+    _blend_fold).  p2p_latent_step builds the mask from them inside the latent-update launch --
+    LocalBlend and the CFG/DDIM step are one kernel per denoising step (null_text.py:41-70,
+    ptp_utils.py:72-75).  materialize() builds the same mask as a uint8 [B, H, W] tensor with
+    p2p_localblend (mixed prompt-group batches, tests)."""
+
+    def __init__(self, maps, heads, alpha_flat, sub_flat, th_pool, th_sub, size, sums):
+        self._maps, self._heads, self._alpha, self._sub = maps, heads, alpha_flat, sub_flat
+        self.th_pool, self.th_sub, self.size, self.sums = float(th_pool), float(th_sub), tuple(size), sums
+
+    def latent_entry(self):
+        """The per-group entry of _hip.latent_step(blend=...)."""
+        return self.sums, self.th_pool, self.th_sub, self._sub is not None
+
+    def materialize(self) -> torch.Tensor:
+        mask = torch.empty(self._alpha.shape[0], *self.size, dtype=torch.uint8, device=self.sums.device)
+        _hip.localblend(self._maps, self._heads, self._alpha, self._sub, self.th_pool, self.th_sub, None, self.sums,
+                        mask_out=mask, word_sums_ready=True)
+        return mask
+
+
+def as_mask(m):
+    """A step mask as a uint8 tensor (materialising a FoldedBlendMask), or None."""
+    return m.materialize() if isinstance(m, FoldedBlendMask) else m
+
+
 def fused_blend_mask(attention_store, alpha_flat, sub_flat, th_pool, th_sub, size, folded=None):
     """LocalBlend's final mask [B, H, W] (uint8) only; the latent blend itself then runs inside
     p2p_latent_step together with the CFG combine and the DDIM step.  ``folded``: the running word
     sums [B, 2, 5 * heads, 256] that the cross-attention store epilogue accumulated
-    (AttentionControlEdit._blend_fold) -- then the 12.6 MB of maps are not re-read."""
+    (AttentionControlEdit._blend_fold) -- then the 12.6 MB of maps are not re-read, and the mask
+    is returned as a FoldedBlendMask that p2p_latent_step builds in the same launch."""
     maps = list(attention_store["down_cross"][2:4]) + list(attention_store["up_cross"][:3])
     B = alpha_flat.shape[0]
     if len(maps) != 5:
         raise ValueError(f"LocalBlend needs 2 down and 3 up 16x16 cross maps, store has {len(maps)}")
     heads = maps[0].shape[0] // B
     dev = maps[0].device
-    mask = torch.empty(B, *size, dtype=torch.uint8, device=dev)
     if folded is not None:
-        _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, None, folded, mask_out=mask,
-                        word_sums_ready=True)
-        return mask
+        return FoldedBlendMask(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, size, folded)
+    mask = torch.empty(B, *size, dtype=torch.uint8, device=dev)
     maps = [m if (m.dtype == torch.float32 and m.is_contiguous()) else m.float().contiguous() for m in maps]
     ws = torch.empty(B * 2 * len(maps) * heads * maps[0].shape[1], dtype=torch.float32, device=dev)
     _hip.localblend(maps, heads, alpha_flat, sub_flat, th_pool, th_sub, None, ws, mask_out=mask)
@@ -676,6 +703,13 @@ class GroupBatch(AttentionControl):
             masks = [fn(size) if fn is not None else None for fn in fns]
             if all(mk is None for mk in masks):
                 return None
+            folded = [mk for mk in masks if isinstance(mk, FoldedBlendMask)]
+            if folded and len(folded) == sum(mk is not None for mk in masks) and \
+                    len({f.latent_entry()[1:] for f in folded}) == 1:
+                # every blending group folded, one threshold set: the masks are built inside
+                # p2p_latent_step (one launch per step for the whole batch)
+                return masks, B
+            masks = [as_mask(mk) for mk in masks]
             dev = next(mk for mk in masks if mk is not None).device
             out = torch.zeros(len(masks) * B, *size, dtype=torch.uint8, device=dev)
             blend = torch.zeros(len(masks), dtype=torch.uint8)

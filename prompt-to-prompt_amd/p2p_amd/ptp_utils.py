@@ -51,14 +51,20 @@ def _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidanc
         return None
     if eps is None or not eps.is_contiguous():
         eps = torch.cat([eps_u, eps_c]).contiguous()
+    from .controllers import FoldedBlendMask
     x = latents.contiguous()
     mask = mask_fn(tuple(x.shape[2:])) if mask_fn is not None else None
-    group_size, group_blend = 0, None
-    if isinstance(mask, tuple):            # prompt-group batch: (mask, group size, groups that blend)
+    group_size, group_blend, blend = 0, None, None
+    if isinstance(mask, FoldedBlendMask):  # LocalBlend built inside the latent-step launch
+        mask, blend = None, [mask.latent_entry()]
+    elif isinstance(mask, tuple) and len(mask) == 2:   # prompt-group batch, every blending group folded
+        blend = [m.latent_entry() if m is not None else None for m in mask[0]]
+        mask, group_size = None, mask[1]
+    elif isinstance(mask, tuple):          # prompt-group batch: (mask, group size, groups that blend)
         mask, group_size, group_blend = mask
     out = torch.empty_like(x)
     return _hip.latent_step(eps, x, out, model.scheduler.prev_coeffs(t), guidance_scale, mask,
-                            group_size, group_blend)
+                            group_size, group_blend, blend)
 
 
 def latent2image(vae, latents):

@@ -30,9 +30,11 @@ def oracle_controller(kind, prompts, tok, steps, dev, local_blend=None, flavour=
     return c
 
 
-def oracle_group(model, prompts, x_T, ctrl, steps=50, guidance=7.5):
+def oracle_group(model, prompts, x_T, ctrl, steps=50, guidance=7.5, uncond_embeddings=None):
     """Final latents [B, 4, h, w] f32 of one edit group; ``ctrl`` (an OracleController) keeps the
-    running-sum store.  x_T: [1, 4, h, w] (init_latent, ptp_utils.py:88-95)."""
+    running-sum store.  x_T: [1, 4, h, w] (init_latent, ptp_utils.py:88-95).  uncond_embeddings:
+    per-step [1, 77, 768] null embeddings (the edit after null-text inversion: the notebook's
+    text2image_ldm_stable call, context_i = cat([uncond_embeddings[i].expand(B, ...), text]))."""
     dev = model.device
     ofw.install(model, ctrl)
     B = len(prompts)
@@ -45,7 +47,10 @@ def oracle_group(model, prompts, x_T, ctrl, steps=50, guidance=7.5):
     ac = sched.alphas_cumprod.to(dev)
     udt = next(model.unet.parameters()).dtype
     with torch.no_grad():
-        for t in sched.timesteps:
+        for i, t in enumerate(sched.timesteps):
+            if uncond_embeddings is not None:
+                text = ctx[B:]
+                ctx = torch.cat([uncond_embeddings[i].to(dev).expand(*text.shape).to(udt), text])
             eps = model.unet(torch.cat([lat] * 2).to(udt), t, encoder_hidden_states=ctx)["sample"].float()
             eu, ec = eps.chunk(2)
             lat = oc.ddim_prev(ac, ac[0], eu + guidance * (ec - eu), int(t), lat, n_inf=steps)

@@ -28,7 +28,7 @@ def _run(model, prompts, fold, masks):
 
         def step_mask(store, size, folded=None):
             m = orig(store, size, folded=folded)
-            masks.append(None if m is None else m.clone())
+            masks.append(None if m is None else controllers.as_mask(m).clone())
             return m
 
         lb.step_mask = step_mask

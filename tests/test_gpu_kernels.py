@@ -318,21 +318,36 @@ def _edit_mapper(B, K, weight=0.5):
     return m
 
 
-@pytest.mark.parametrize("geom", [(4096, 40, 77), (1024, 80, 77), (256, 160, 77), (64, 160, 77), (100, 80, 96),
-                                  (333, 40, 33)], ids=lambda g: "x".join(map(str, g)))
-@pytest.mark.parametrize("n_groups", [1, 2])
-def test_cross_group_kernel_bf16(cuda, geom, n_groups):
-    """The group-coupled cross kernel (bf16 inputs: p2p_cross.hip): [uncond groups | cond groups],
-    each cond group a source + 3 dense Replace edits against its OWN source (main.py:185-193), the
-    cond maps kept and accumulated over two calls, LocalBlend word sums folded in, against fp32
-    einsum on the same bf16 inputs.  Covers G1-G4, ragged P, K = 96 (no short tail), K = 33."""
+# (P, d, K, heads, prompt groups, kernel the launch must dispatch to): run_cross takes
+# cross_group_kernel only when n_groups x heads x ceil(P / 128) >= 512 (p2p_cross.hip
+# cross_group_eligible), so the group-kernel cases are sized to clear that bar
+CROSS_GROUP_CASES = [
+    (4096, 40, 77, 8, 1, "group"), (4096, 40, 77, 8, 2, "group"),     # G1/G7
+    (1024, 80, 77, 8, 4, "group"),                                    # G2/G6 as configs[3] batches it
+    (1000, 80, 77, 8, 4, "group"),                                    # ragged P (rows past P in the store RMW)
+    (1000, 80, 96, 8, 4, "group"),                                    # K = 96: no short key tail
+    (4000, 40, 33, 8, 1, "group"),                                    # K = 33, ragged P
+    (256, 160, 77, 16, 8, "group"),                                   # d = 160 (16 heads to reach the bar)
+    (1024, 80, 77, 8, 1, "entry"), (256, 160, 77, 8, 2, "entry"),     # G2-G4 at configs[1]: per-entry
+    (64, 160, 77, 8, 1, "entry"), (100, 80, 96, 8, 2, "entry"), (333, 40, 33, 8, 1, "entry"),
+]
+
+
+@pytest.mark.parametrize("case", CROSS_GROUP_CASES, ids=lambda c: "P{}_d{}_K{}_H{}_g{}_{}".format(*c))
+def test_cross_group_kernel_bf16(cuda, case):
+    """The cross-attention kernels with bf16 inputs (p2p_cross.hip group kernel where the grid is
+    large enough, cross_attn_kernel otherwise; the case states which and the test asserts the
+    dispatch rule): [uncond groups | cond groups], each cond group a source + 3 dense Replace
+    edits against its OWN source (main.py:185-193), the cond maps kept and accumulated over two
+    calls, LocalBlend word sums folded in, against fp32 einsum on the same bf16 inputs.  The group
+    kernel is covered at d = 40 / 80 / 160, ragged P, K = 96 (no short tail) and K = 33."""
     from p2p_amd import programs
-    P, d, K = geom
-    B, H = 4, 8
+    P, d, K, H, n_groups, kernel = case
+    B = 4
     N = 2 * B * n_groups
     q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=6.0, seed=31 + P)
     scale = d ** -0.5
-    mappers = [_edit_mapper(B, K), _edit_mapper(B, K).flip(0)][:n_groups]
+    mappers = [_edit_mapper(B, K) if g % 2 == 0 else _edit_mapper(B, K).flip(0) for g in range(n_groups)]
     progs = [programs.replace_program(m).to_device(cuda) for m in mappers]
     alpha = torch.ones(B - 1, K, device=cuda)      # edit 0: alpha 1 everywhere (R only)
     alpha[1] = 0.0                                   # edit 1: alpha 0 everywhere (own P only)
@@ -348,6 +363,8 @@ def test_cross_group_kernel_bf16(cuda, geom, n_groups):
     store = torch.zeros(BG * H, P, K, device=cuda)
     slots = [-1] * BG + [i * H for i in range(BG)]
     o = torch.empty_like(q)
+    t = _hip.make_tensors(q, k, v, o, H, scale, "bf16")
+    assert _hip.cross_group_dispatch(t, groups) == (kernel == "group")
     for acc in (False, True):
         _hip.cross_attn(q, k, v, o, H, scale, groups, store=store, store_slot=slots, accumulate=acc)
     p = ref_probs(q, k, H, scale)                                    # [N, H, P, K]

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import control as oc
-from p2p_amd import _hip
+from p2p_amd import _hip, controllers
 from p2p_amd.ddim import DDIMScheduler
 
 pytestmark = pytest.mark.gpu
@@ -102,3 +102,45 @@ def test_mask_only_localblend_matches_full(cuda):
     plain = _hip.latent_step(eps, x, torch.empty_like(x), coeffs, 7.5, None)
     _hip.localblend(maps, H, alpha, None, 0.3, 0.3, plain, ws)
     assert torch.equal(fused, plain)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("sub", [False, True], ids=["nosub", "substruct"])
+@pytest.mark.parametrize("groups", [(True,), (True, False, True)], ids=["one_group", "three_groups"])
+def test_latent_step_builds_folded_blend_mask(cuda, dtype, sub, groups):
+    """LocalBlend in the latent-update launch (p2p_latent_step with blend sums, one kernel per
+    step): bit-identical to building the mask from the same folded word sums with
+    p2p_localblend (word_sums_ready) and blending with it in the mask-reading latent step."""
+    gs, H, L = 4, 8, 5
+    G = len(groups)
+    B = G * gs
+    g = torch.Generator(device=cuda).manual_seed(17 + G + 2 * sub)
+    eps = torch.randn(2 * B, 4, 64, 64, device=cuda, generator=g).to(dtype)
+    x = torch.randn(B, 4, 64, 64, device=cuda, generator=g)
+    coeffs = sched().prev_coeffs(500)
+    maps = [torch.zeros(gs * H, 256, 77, device=cuda) for _ in range(L)]   # not read (word sums ready)
+    alpha = torch.ones(gs, 77, device=cuda)
+    subt = torch.ones(gs, 77, device=cuda) if sub else None
+    blend, masks = [], []
+    for gi, on in enumerate(groups):
+        # smooth-ish positive word sums, so the pooled maps cross the thresholds in many places
+        # (one spatial field per prompt shared by its L*H maps, with per-map noise: the mean over
+        # the maps keeps the field's structure)
+        base = torch.rand(gs * 2, 1, 4, 4, device=cuda, generator=g) ** 3
+        field = torch.nn.functional.interpolate(base, size=(16, 16), mode="bilinear", align_corners=False)
+        sums = field.reshape(gs, 2, 1, 256) * (0.8 + 0.4 * torch.rand(gs, 2, L * H, 256, device=cuda, generator=g))
+        sums = sums.contiguous()
+        if not sub:
+            sums[:, 1] = 0
+        fm = controllers.FoldedBlendMask(maps, H, alpha, subt, 0.5, 0.45, (64, 64), sums)
+        blend.append(fm.latent_entry() if on else None)
+        masks.append(fm.materialize() if on else torch.zeros(gs, 64, 64, dtype=torch.uint8, device=cuda))
+    got = _hip.latent_step(eps, x, torch.empty_like(x), coeffs, 7.5, None, gs if G > 1 else 0, None, blend)
+    gb = torch.tensor([1 if on else 0 for on in groups], dtype=torch.uint8, device=cuda)
+    want = _hip.latent_step(eps, x, torch.empty_like(x), coeffs, 7.5, torch.cat(masks), gs if G > 1 else 0,
+                            gb if G > 1 else None)
+    frac = torch.cat(masks).float().mean().item()
+    assert 0.05 < frac < 0.95, frac        # the masks are neither empty nor full
+    assert torch.equal(got, want), (got - want).abs().max().item()
+    with pytest.raises(_hip.HipError):      # out may not alias x in the fused form
+        _hip.latent_step(eps, x, x, coeffs, 7.5, None, gs if G > 1 else 0, None, blend)
