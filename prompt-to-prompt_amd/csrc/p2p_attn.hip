@@ -1252,31 +1252,47 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // (two loads per lane cover 32 rows of up to 96 keys; their values are only consumed at the very
   // end, so nothing waits for them)
   float touch0 = 0.f, touch1 = 0.f;
-  if (stored && a.store_accumulate) {
-    const int rows = min(32, a.P - p0w);
-    const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
-    const int lines = (rows * K * 4 + 127) / 128;
-    static_assert(32 * P2P_MAX_KEYS_CROSS * 4 / 128 <= 128, "two touches per lane");
-    if (lane < lines) touch0 = g[lane * 32];
-    if (lane + 64 < lines) touch1 = g[(lane + 64) * 32];
-  }
-  // LocalBlend word weights of this entry (lanes 0-31: alpha, 32-63: substruct) into LDS now; the
-  // store epilogue's per-row word sums then read them from LDS, not global memory
-  __shared__ float btab[2][P2P_MAX_KEYS_CROSS];
+  // LocalBlend word weights of this entry (lanes 0-31: alpha, 32-63: substruct) for LDS: loaded now
+  // (unconditionally, from valid addresses: a load inside a branch gets its own wait), written to
+  // LDS once the prologue's loads are in flight; the store epilogue's per-row word sums then read
+  // them from LDS, not global memory
+  __shared__ __attribute__((aligned(16))) float btab[2][P2P_MAX_KEYS_CROSS];
   const bool blend_on = stored && a.grp_bsum[gi] != nullptr;
+  float bw0 = 0.f, bw1 = 0.f;
   if (blend_on) {
     const float* const ta = a.grp_balpha[gi] + (int64_t)b * K;
     const float* const tsub = a.grp_bsub[gi];
     static_assert(2 * P2P_MAX_KEYS_CROSS <= 2 * NT, "two weights per thread");
-    float w0 = 0.f, w1 = 0.f;
     const int i1 = tid + NT;
-    if (tid < K) w0 = ta[tid];
-    else if (tid < 2 * K && tsub != nullptr) w0 = tsub[(int64_t)b * K + tid - K];
-    if (i1 < K) w1 = ta[i1];
-    else if (i1 < 2 * K && tsub != nullptr) w1 = tsub[(int64_t)b * K + i1 - K];
-    if (tid < 2 * K) btab[tid < K ? 0 : 1][tid < K ? tid : tid - K] = w0;
-    if (i1 < 2 * K) btab[i1 < K ? 0 : 1][i1 < K ? i1 : i1 - K] = w1;
+    const float* s0 = tid < K ? ta + tid : (tid < 2 * K && tsub != nullptr) ? tsub + (int64_t)b * K + tid - K : ta;
+    const float* s1 = i1 < K ? ta + i1 : (i1 < 2 * K && tsub != nullptr) ? tsub + (int64_t)b * K + i1 - K : ta;
+    bw0 = *s0;
+    bw1 = *s1;
+    if (!(tid < K || (tid < 2 * K && tsub != nullptr))) bw0 = 0.f;
+    if (!(i1 < K || (i1 < 2 * K && tsub != nullptr))) bw1 = 0.f;
   }
+  // once the prologue's loads are issued: the blend weights into LDS, and this wave's rows of the
+  // running sum touched into this XCD's L2 (32 x K f32, contiguous; two loads per lane cover 32
+  // rows of up to 96 keys) so the store epilogue's read-add-write finds them there.  The touches
+  // go last: they miss to HBM, and a wait for any load issued after them would wait for them too
+  auto finish_prologue = [&]() __attribute__((always_inline)) {
+    if (blend_on) {
+      const int i1 = tid + NT;
+      if (tid < 2 * K) btab[tid < K ? 0 : 1][tid < K ? tid : tid - K] = bw0;
+      if (i1 < 2 * K) btab[i1 < K ? 0 : 1][i1 < K ? i1 : i1 - K] = bw1;
+      // columns K.. of both tables are zero (the 16-byte weight reads of the register sums)
+      for (int i = tid; i < 2 * (P2P_MAX_KEYS_CROSS - K); i += NT)
+        btab[i / (P2P_MAX_KEYS_CROSS - K)][K + i % (P2P_MAX_KEYS_CROSS - K)] = 0.f;
+    }
+    if (stored && a.store_accumulate) {
+      const int rows = min(32, a.P - p0w);
+      const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
+      const int lines = (rows * K * 4 + 127) / 128;
+      static_assert(32 * P2P_MAX_KEYS_CROSS * 4 / 128 <= 128, "two touches per lane");
+      if (lane < lines) touch0 = g[lane * 32];
+      if (lane + 64 < lines) touch1 = g[(lane + 64) * 32];
+    }
+  };
 
   // padding the MFMAs read but the staging never writes (disjoint from it: no extra barrier):
   // K columns D..DK (multiplied by Q's zero columns) and V rows K..KR (weighted by p = 0)
@@ -1401,6 +1417,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // the workgroup waits one memory round trip instead of two (variant 138 of an experiments
   // build: own K / V staged after the R phase, as before)
   Chunk8<IO> kc1[kDenseOk ? NCH : 1], vc1[kDenseOk ? NCH : 1];
+  typename MQ::frag qf1[kDenseOk ? NKT : 1];   // (and its own Q rows)
   bool own_early = false;
   if constexpr (kDenseOk) {
    if (dense) {
@@ -1435,7 +1452,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
 #ifdef P2P_EXPERIMENTS
     if (a.variant == 138) own_early = false;
 #endif
-    if (own_early) load_kv(n, kc1, vc1, true);
+    if (own_early) {
+      load_kv(n, kc1, vc1, true);
+      load_q(n, qf1);
+    }
+    finish_prologue();
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const int i = tid + j * NT;
@@ -1492,7 +1513,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       }
     }
     }
-    load_q(n, qf);
+    if (own_early) {
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) qf[t] = qf1[t];
+    } else {
+      load_q(n, qf);
+    }
     __syncthreads();  // every wave is done with the source K tile and the mapper tile
     P2P_CROSS_STAMP(10)
    }
@@ -1500,7 +1526,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   if (edit && !dense) {
     // ---- source probabilities P0 for these rows -> this wave's LDS slab
     load_q(first, qf);
-    stage(first, false);
+    {
+      Chunk8<IO> kc[NCH], vc[NCH];
+      load_kv(first, kc, vc, false);
+      finish_prologue();
+      store_kv(kc, vc, false);
+    }
     __syncthreads();
     probs(qf, sv);
     load_q(n, qf);
@@ -1515,11 +1546,17 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   } else if (!edit) {
     load_q(n, qf);
   }
+  auto stage_own = [&]() __attribute__((always_inline)) {
+    Chunk8<IO> kc[NCH], vc[NCH];
+    load_kv(n, kc, vc, true);
+    if (!edit) finish_prologue();   // (the edit paths called it with their first loads)
+    store_kv(kc, vc, true);
+  };
   if constexpr (kDenseOk) {
     if (own_early) store_kv(kc1, vc1, true);
-    else stage(n, true);
+    else stage_own();
   } else {
-    stage(n, true);
+    stage_own();
   }
   __syncthreads();
   P2P_CROSS_STAMP(11)
@@ -1610,18 +1647,37 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     P2P_CROSS_STAMP(17)
     const int rows = min(32, a.P - p0w);
-    // LocalBlend's word sums of these rows (lanes 0-31: alpha, 32-63: substruct), folded here so
-    // the blend never re-reads the maps; words summed in index order as blend_wordsum_kernel does
-    if (blend_on && qi < rows) {
-      float acc = 0.f;
-      if ((hh == 0 ? a.grp_balpha[gi] : a.grp_bsub[gi]) != nullptr) {
-        const float* tab = btab[hh];
-        const float* row = slab + qi * K;
-#pragma unroll 8
-        for (int w = 0; w < K; ++w) acc += row[w] * tab[w];   // one sequential chain: the reads run ahead
+    // LocalBlend's word sums of these rows (alpha- and substruct-weighted), folded here so the
+    // blend never re-reads the maps: each lane sums the words it holds in registers (runs of four
+    // consecutive words, weights read 16 bytes at a time), the two lane halves of a row add, and
+    // lanes 0-31 write the alpha sum, 32-63 the substruct sum.  (A pairwise order instead of
+    // blend_wordsum_kernel's sequential one: the fold is already a measured summation-order
+    // deviation from the map path; the sequential chain cost ~3k cycles per workgroup.)
+    if (blend_on) {
+      const bool has_sub = a.grp_bsub[gi] != nullptr;
+      float sa = 0.f, ss = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int w0 = kb * 32 + 8 * g4 + 4 * hh;
+          if (w0 >= K) continue;   // (btab is zero past K: the run that straddles K adds zeros)
+          const f32x4_t ta = *reinterpret_cast<const f32x4_t*>(&btab[0][w0]);
+          const f32x4_t ts = *reinterpret_cast<const f32x4_t*>(&btab[1][w0]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float pv = w0 + j < K ? sv[kb][4 * g4 + j] : 0.f;
+            sa = fmaf(pv, ta[j], sa);
+            ss = fmaf(pv, ts[j], ss);
+          }
+        }
+      sa += other_half(sa);
+      ss += other_half(ss);
+      if (qi < rows) {
+        const float acc = hh == 0 ? sa : (has_sub ? ss : 0.f);
+        float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w + qi;
+        *dst = a.store_accumulate ? *dst + acc : acc;
       }
-      float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w + qi;
-      *dst = a.store_accumulate ? *dst + acc : acc;
     }
     P2P_CROSS_STAMP(18)
     if (rows > 0) {

@@ -10,6 +10,8 @@
 //   x_t    = x_t[:1] + mask * (x_t - x_t[:1])
 // Kernel 1 reduces the word axis for every (prompt, layer x head) map; kernel 2 does the rest,
 // one workgroup per prompt (each rebuilds prompt 0's mask, which gates every other prompt).
+#include <type_traits>
+
 #include "p2p_device.h"
 #include "p2p_kernels.h"
 
@@ -101,36 +103,46 @@ __device__ __forceinline__ int blend_src_of(int yx, int R, int lat_h, int lat_w)
 // thresholds, mask[:1] | mask, substruct gate (null_text.py:41-67).  Called by all 256 threads of
 // the workgroup (it synchronises); blend_finalize_kernel and latent_blend_kernel share it, so
 // both build the same mask bit for bit.
-__device__ void build_blend_mask(const float* ws0, const float* wsb, int LH, int R, int lat_h, int lat_w,
+__device__ __forceinline__ void build_blend_mask(const float* ws0, const float* wsb, int LH, int R, int lat_h, int lat_w,
                                  float th_pool, float th_sub, bool sub, BlendLds& L) {
   const int R2 = R * R;
   const int tid = threadIdx.x;
-  // mean over the L*H maps (sum in index order, then / L*H as Tensor.mean does)
-  for (int i = tid; i < 2 * R2; i += 256) {
-    const int k = i / R2, pix = i - k * R2;
-    const float* wa = (k ? wsb : ws0) + pix;
-    const float* ws = (k ? wsb : ws0) + (int64_t)LH * R2 + pix;
-    float sa = 0.f, ss = 0.f;
-    // every load in flight at once (the five blended 16x16 layers x 8 heads = 40 maps: one memory
-    // round trip instead of three), then the in-order sums
-    constexpr int kBatch = 48;
-    for (int j0 = 0; j0 < LH; j0 += kBatch) {
-      float va[kBatch], vs[kBatch];
+  // mean over the L*H maps (sum in index order, then / L*H as Tensor.mean does).  The four
+  // (prompt, sum) planes -- source / b x alpha / substruct -- go to the four waves; a lane sums
+  // four adjacent map pixels, so every load is one 16-byte row piece and a wave's LH loads of a
+  // plane are all in flight at once (one memory round trip for the whole mask)
+  {
+    const int g = tid >> 6, k = g & 1, sidx = g >> 1;     // (source | b) x (alpha | substruct)
+    const int px0 = (tid & 63) * 4;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (px0 < R2 && (sidx == 0 || sub)) {
+      const float* base = (k ? wsb : ws0) + (int64_t)sidx * LH * R2;
+      if ((R2 & 3) == 0) {
+        // buffer loads: maps past LH read as 0 (range-checked), so the 48 loads of a batch are
+        // issued unconditionally, all before the first add; adding those +0.0 to a sum of
+        // non-negative terms leaves it bit for bit (the in-order sum over j < LH)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, (int64_t)LH * R2 * 4);
+        for (int j0 = 0; j0 < LH; j0 += 48) {
+          f32x4_t v[48];
 #pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        const int j = min(j0 + u, LH - 1);
-        va[u] = wa[(int64_t)j * R2];
-        vs[u] = sub ? ws[(int64_t)j * R2] : 0.f;
-      }
+          for (int u = 0; u < 48; ++u)
+            v[u] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j0 + u) * R2 + px0) * 4, 0, 0));
 #pragma unroll
-      for (int u = 0; u < kBatch; ++u)
-        if (j0 + u < LH) {
-          sa += va[u];
-          ss += vs[u];
+          for (int u = 0; u < 48; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] += v[u][q];
         }
+      } else {
+        for (int j = 0; j < LH; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (px0 + q < R2) acc[q] += base[(int64_t)j * R2 + px0 + q];
+      }
     }
-    L.mean_a[k][pix] = sa / (float)LH;
-    L.mean_s[k][pix] = ss / (float)LH;
+    float* const dst = sidx == 0 ? L.mean_a[k] : L.mean_s[k];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (px0 + q < R2) dst[px0 + q] = acc[q] / (float)LH;
   }
   __syncthreads();
   // 3x3 max-pool, stride 1, padding 1 (padding never wins: -inf)
@@ -185,7 +197,7 @@ __device__ void build_blend_mask(const float* ws0, const float* wsb, int LH, int
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void blend_finalize_kernel(p2p_blend_args a) {
+__global__ __launch_bounds__(256, 1) void blend_finalize_kernel(p2p_blend_args a) {
   const int b = blockIdx.x;
   const int R = a.map_res;
   const int R2 = R * R;
@@ -236,8 +248,19 @@ __device__ __forceinline__ float sub_rn(float a, float b) { return __fsub_rn(a, 
 
 // prev_sample from one element's inputs (CFG combine + DDIM step): eu / ec the unconditional and
 // conditional eps (ec unused without CFG), x the latent
-template <bool BF16>
-__device__ __forceinline__ float ddim_from(const p2p_latent_step_args& a, float eu, float ec, float x) {
+// the step's scalar coefficients, copied out of the kernel-argument struct by value (a kernel that
+// also indexes the struct's blend_sums[] array at run time would otherwise read every field through
+// a vector load of the kernarg segment, one dependent round trip each)
+struct DdimC {
+  int cfg;
+  float guidance, sqrt_beta_t, sqrt_alpha_t, sqrt_alpha_prev, sqrt_one_minus_alpha_prev;
+  __device__ explicit DdimC(const p2p_latent_step_args& a)
+      : cfg(a.cfg), guidance(a.guidance), sqrt_beta_t(a.sqrt_beta_t), sqrt_alpha_t(a.sqrt_alpha_t),
+        sqrt_alpha_prev(a.sqrt_alpha_prev), sqrt_one_minus_alpha_prev(a.sqrt_one_minus_alpha_prev) {}
+};
+
+template <bool BF16, typename A>
+__device__ __forceinline__ float ddim_from(const A& a, float eu, float ec, float x) {
   auto rd = [](float v) { return BF16 ? rnd_bf16(v) : v; };
   float noise;
   if (a.cfg) {
@@ -294,60 +317,79 @@ __global__ __launch_bounds__(256) void latent_step_kernel(p2p_latent_step_args a
 }
 
 // The latent step with LocalBlend's mask built in the same launch (a.blend_sums): grid
-// (pixel chunks, prompts).  A workgroup of an edit prompt b whose group blends builds b's mask
-// per map pixel from the folded word sums (build_blend_mask: ~160 KB of L2-resident sums) and
-// updates its chunk of b's latent -- recomputing the group source's prev_sample, which it blends
-// towards, from the same inputs (bit-identical to the source workgroup's).  No workgroup reads
-// another's output.  The kernel is latency-bound (1 MB per step): every thread issues all its
-// eps / x loads (kPxT pixels x up to 4 channels, for b and the source) before the mask build's
-// loads, so the whole launch waits about two memory round trips.
+// (pixel chunks of 256, prompts).  A workgroup of an edit prompt b whose group blends builds b's
+// mask per map pixel from the folded word sums (build_blend_mask: ~160 KB of L2-resident sums, one
+// round trip) and updates its chunk of b's latent -- recomputing the group source's prev_sample,
+// which it blends towards, from the same inputs (bit-identical to the source workgroup's).  No
+// workgroup reads another's output.  The kernel is latency-bound (1 MB per step): every thread
+// issues its eps / x loads (4 pixels x 1 channel, for b and the source) before the mask build's,
+// so the launch waits about two memory round trips; 64 workgroups keep the per-thread DDIM
+// arithmetic (two IEEE divisions per element) short.
 template <bool BF16>
-__global__ __launch_bounds__(256) void latent_blend_kernel(p2p_latent_step_args a, int64_t chw, int px_per_wg) {
-  constexpr int kPxT = 4;     // latent pixels per thread
-  constexpr int kCg = 4;      // channels per pass (SD latents: 4)
+__global__ __launch_bounds__(256, 1) void latent_blend_kernel(p2p_latent_step_args a, int64_t chw, int px_per_wg) {
+  // every field this kernel reads, copied to scalars first (see DdimC)
   const int HW = a.height * a.width;
   const int b = blockIdx.y;
-  const int gs = a.group_size > 0 ? a.group_size : a.n_prompts;
+  const int NP = a.n_prompts, C = a.channels, H = a.height, W = a.width;
+  const int gs = a.group_size > 0 ? a.group_size : NP;
   const int g = b / gs, bg = b - g * gs, b0 = b - bg;
-  const float* ws = a.blend_sums[g];
+  const float* const ws = a.blend_sums[g];
+  const float* const xg = a.x;
+  const void* const eg = a.eps;
+  float* const og = a.out;
+  const int lh = a.blend_lh, res = a.blend_res, use_sub = a.blend_sub;
+  const float th_pool = a.blend_th_pool, th_sub = a.blend_th_sub;
+  const DdimC dc(a);
   const bool blend = bg != 0 && ws != nullptr;          // workgroup-uniform
   __shared__ BlendLds L;
-  const int px = blockIdx.x * px_per_wg + threadIdx.x * kPxT;
-  for (int c0 = 0; c0 < a.channels; c0 += kCg) {
-    float eu[2][kCg][kPxT], ec[2][kCg][kPxT], xv[2][kCg][kPxT];
-    // every load of this pass first (the source's only when blending)
+  // a workgroup covers px_per_wg = 256 pixels x 4 channels per pass: thread t takes channel
+  // c0 + t / 64 and 4 adjacent pixels (16-byte pieces; HW % 4 == 0, checked by the launcher)
+  const int px = blockIdx.x * px_per_wg + (threadIdx.x & 63) * 4;
+  const int pxc = min(px, HW - 4);
+  // raw loads first, unconditionally (clamped to valid addresses; the unused ones are discarded),
+  // so no load sits in a branch with its own wait: every load of the pass is in flight at once
+  using Raw = typename std::conditional<BF16, uint2, f32x4_t>::type;
+  auto ld_eps = [eg](int64_t idx) __attribute__((always_inline)) -> Raw {
+    if constexpr (BF16) return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(eg) + idx);
+    else return *reinterpret_cast<const f32x4_t*>(static_cast<const float*>(eg) + idx);
+  };
+  auto unpack = [](const Raw& r) __attribute__((always_inline)) -> f32x4_t {
+    if constexpr (BF16)
+      return f32x4_t{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                     __uint_as_float(r.y & 0xffff0000u)};
+    else return r;
+  };
+  for (int c0 = 0; c0 < C; c0 += 4) {
+    const int c = c0 + (threadIdx.x >> 6);
+    const int64_t i = (int64_t)min(c, C - 1) * HW + pxc;
+    Raw reu[2], rec[2];
+    f32x4_t xv[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const int bb = s2 ? b0 : b;
-#pragma unroll
-      for (int c = 0; c < kCg; ++c)
-#pragma unroll
-        for (int j = 0; j < kPxT; ++j) {
-          const bool live = (s2 == 0 || blend) && c0 + c < a.channels && px + j < HW;
-          const int64_t i = (int64_t)(c0 + c) * HW + px + j;
-          eu[s2][c][j] = live ? eps_at<BF16>(a, (int64_t)bb * chw + i) : 0.f;
-          ec[s2][c][j] = live && a.cfg ? eps_at<BF16>(a, (int64_t)(a.n_prompts + bb) * chw + i) : 0.f;
-          xv[s2][c][j] = live ? a.x[(int64_t)bb * chw + i] : 0.f;
-        }
+      reu[s2] = ld_eps((int64_t)bb * chw + i);
+      rec[s2] = ld_eps((int64_t)((dc.cfg ? NP : 0) + bb) * chw + i);
+      xv[s2] = *reinterpret_cast<const f32x4_t*>(xg + (int64_t)bb * chw + i);
     }
     if (blend && c0 == 0) {
-      const int R2 = a.blend_res * a.blend_res;
-      build_blend_mask(ws, ws + (int64_t)bg * 2 * a.blend_lh * R2, a.blend_lh, a.blend_res, a.height, a.width,
-                       a.blend_th_pool, a.blend_th_sub, a.blend_sub != 0, L);
+      const int R2 = res * res;
+      build_blend_mask(ws, ws + (int64_t)bg * 2 * lh * R2, lh, res, H, W, th_pool, th_sub, use_sub != 0, L);
     }
+    if (c >= C || px >= HW) continue;
+    const f32x4_t eu = unpack(reu[0]), ec = unpack(rec[0]);
+    f32x4_t o;
 #pragma unroll
-    for (int c = 0; c < kCg; ++c)
-#pragma unroll
-      for (int j = 0; j < kPxT; ++j) {
-        if (c0 + c >= a.channels || px + j >= HW) continue;
-        float prev = ddim_from<BF16>(a, eu[0][c][j], ec[0][c][j], xv[0][c][j]);
-        if (blend) {
-          const float prev0 = ddim_from<BF16>(a, eu[1][c][j], ec[1][c][j], xv[1][c][j]);
-          const float m = L.msrc[blend_src_of(px + j, a.blend_res, a.height, a.width)];
-          prev = add_rn(prev0, mul_rn(m, sub_rn(prev, prev0)));
-        }
-        a.out[(int64_t)b * chw + (int64_t)(c0 + c) * HW + px + j] = prev;
+    for (int j = 0; j < 4; ++j) {
+      float prev = ddim_from<BF16>(dc, eu[j], ec[j], xv[0][j]);
+      if (blend) {
+        const f32x4_t eu0 = unpack(reu[1]), ec0 = unpack(rec[1]);
+        const float prev0 = ddim_from<BF16>(dc, eu0[j], ec0[j], xv[1][j]);
+        const float m = L.msrc[blend_src_of(px + j, res, H, W)];
+        prev = add_rn(prev0, mul_rn(m, sub_rn(prev, prev0)));
       }
+      o[j] = prev;
+    }
+    *reinterpret_cast<f32x4_t*>(og + (int64_t)b * chw + (int64_t)c * HW + px) = o;
   }
 }
 
@@ -368,10 +410,11 @@ int run_latent_step(const p2p_latent_step_args& a, hipStream_t st) {
   if (fused) {
     // the mask comes from the word sums; a precomputed mask as well would be ambiguous.  out must
     // not alias x: a source workgroup's writes would race with the edit workgroups' reads of x[g0]
-    if (a.mask || a.group_blend || a.out == a.x || a.blend_lh < 1 || a.blend_res < 1 ||
+    if (a.mask || a.group_blend || a.out == a.x || a.blend_lh < 1 || a.blend_res < 1 || (a.height * a.width) % 4 ||
+        ((uintptr_t)a.x | (uintptr_t)a.out | (uintptr_t)a.eps) % 16 ||
         a.blend_res * a.blend_res > 256 || a.blend_res > a.height || a.blend_res > a.width)
       return P2P_E_ARG;
-    constexpr int kPx = 1024;   // latent pixels per workgroup: 256 threads x 4
+    constexpr int kPx = 256;    // latent pixels per workgroup (x 4 channels: 256 threads x 4 elements)
     const int hw = a.height * a.width;
     dim3 grid((hw + kPx - 1) / kPx, a.n_prompts);
     if (a.eps_dtype == P2P_DTYPE_BF16)

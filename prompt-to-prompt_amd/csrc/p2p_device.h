@@ -379,6 +379,18 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// One global_load_lds_dwordx4 (16 bytes per lane into LDS at lds_off + lane * 16), as inline asm
+// so hipcc does not track it: its own bookkeeping would drain every in-flight DMA with vmcnt(0)
+// before the next LDS read of the ring (it cannot tell the stages apart).  The ring's waits are
+// the explicit counted vmcnt below; the compiler's own waits only grow stricter with these newer
+// operations in the in-order counter.  (cdna_hip_programming.md, the m0 recipe.)
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_off) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_off)
+               : "memory");
+}
 // The value held by lane l ^ 32 (the other half of the wave), via v_permlane32_swap: no LDS
 // round trip (ds_bpermute) on the softmax critical path.
 __device__ __forceinline__ float other_half(float x) {

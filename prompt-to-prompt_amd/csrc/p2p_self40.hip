@@ -134,6 +134,19 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int kWe = !kFlagSync ? X : (FORM & 262144) ? (3 * X) / 4 : X / 2;
   static_assert(kWe > kWs, "staging window");
   auto nchunks = [](auto role) { return decltype(role)::value == 0 ? NCH : SCH; };
+  // FORM bit 1048576 (DMA staging, bf16 form only): K / V tiles go global -> LDS by
+  // global_load_lds (no staging VGPRs, no staging VALU, no LDS write instructions): the next tile's
+  // DMA is issued at the top of a tile into the other buffer and waited (vmcnt(0)) before the tile
+  // barrier.  The DMA writes whole 16-byte slots of every LDS row, padding included, so V's row-sum
+  // column D cannot live in the tile: the P V operand's columns D.. come from a constant [4][16]
+  // block (column 0 = 1, the rest 0) instead.  With the key split (bit 524288) this is the d = 80
+  // kernel with two waves per SIMD that register staging could not fit in 256 VGPRs.
+  constexpr bool kDma = (FORM & 1048576) != 0;
+  static_assert(!kDma || (!kF16 && kDK == kD && (kDV - kD) <= 16), "DMA staging: bf16 form, no K padding read");
+  constexpr int KSL = kKS / 8, VSL = kVS / 8;   // 16-byte slots per K / V row in LDS
+  constexpr int kDmaK = BK * KSL / 64, kDmaV = BK * VSL / 64;   // DMA instructions per tile
+  static_assert(!kDma || ((BK * KSL) % 64 == 0 && (BK * VSL) % 64 == 0), "whole DMA instructions per tile");
+  __shared__ __attribute__((aligned(16))) uint16_t vones[kDma ? 64 : 8];
   // K and V tile buffers; after the last tile the same LDS holds each wave's output rows (epilogue)
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KBUF + 2 * VBUF];
   uint16_t* const Ks = smem;
@@ -194,12 +207,22 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       *reinterpret_cast<short8_t*>(Vs + r * kVS + kD + 8 * j) =
           short8_t{(short)(j == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
   }
+  if constexpr (kDma)
+    if (tid < 64) vones[tid] = (tid & 15) == 0 ? (uint16_t)0x3F80 : (uint16_t)0;   // [4][16]: column 0 = 1
   if (tid == 0) wg_flag = 0;
   if constexpr (kFlagSync)
     if (tid < 4) tsync[tid] = 0;
 
   // ---- Q fragments: lane (qi, hh) of block b, k step t holds Q[p][16t + 8hh .. +7]
   bool ovf = false;
+  // FORM bit 8388608: K's f16 range check as a running packed u16 maximum of the bf16 magnitudes
+  // (v_and + v_pk_max_u16 per pair), compared once at the end: a bf16 magnitude >= 0x4780 (65536,
+  // past the f16 range; inf / NaN included) sends the workgroup to the exact path -- instead of an
+  // f32 |x| maximum per chunk (the fmaxf NaN canonicalisation made that ~3.5 VALU per pair)
+  constexpr bool kU16Max = (FORM & 8388608) != 0;
+  typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  u16x2_t kmag = {0, 0};
   short8_t qf[QB][kNKT];
   auto load_q = [&](bool prescale) __attribute__((always_inline)) {
 #pragma unroll
@@ -282,7 +305,18 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       return;
     }
     uint16_t* const kd = Ks + buf * KBUF + lrow[i] * kKS + lch[i] * 8;
-    if (as_f16) {
+    if (as_f16 && kU16Max) {
+      const u32x4_t wv = __builtin_bit_cast(u32x4_t, kreg[i]);
+      u32x4_t hv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t w = wv[j];
+        kmag = __builtin_elementwise_max(kmag, __builtin_bit_cast(u16x2_t, w & 0x7fff7fffu));
+        hv[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__uint_as_float(w << 16),
+                                                                       __uint_as_float(w & 0xffff0000u)));
+      }
+      *reinterpret_cast<u32x4_t*>(kd) = hv;
+    } else if (as_f16) {
       short8_t hv;
       float mx = 0.f;
 #pragma unroll
@@ -312,6 +346,34 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     else go(std::integral_constant<int, 1>{});
   };
 
+  // DMA of tile kt into buffer buf: instruction i (of kDmaK K + kDmaV V) moves 64 16-byte slots;
+  // wave w issues i = w, w + WAVES, ...  Padding slots fetch a valid chunk of the same row, rows
+  // past K the last key (finite data; their scores are masked, their P is 0)
+  const uint32_t smem_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto dma_tile = [&](int kt, int buf) __attribute__((always_inline)) {
+    if constexpr (kDma) {
+      const int w0 = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+      for (int j = 0; j < (kDmaK + kDmaV + WAVES - 1) / WAVES; ++j) {
+        const int i = w0 + j * WAVES;
+        if (i < kDmaK) {
+          const int slot = i * 64 + lane;
+          const int row = slot / KSL;
+          const int ch = min(slot - row * KSL, kCPR - 1);
+          const int key = min(kt * BK + row, K - 1);
+          glds16(kp + (int64_t)key * a.ldk + ch * 8,
+                 __builtin_amdgcn_readfirstlane(smem_lds + (uint32_t)(buf * KBUF * 2 + i * 1024)));
+        } else if (i < kDmaK + kDmaV) {
+          const int slot = (i - kDmaK) * 64 + lane;
+          const int row = slot / VSL;
+          const int ch = min(slot - row * VSL, kCPR - 1);
+          const int key = min(kt * BK + row, K - 1);
+          glds16(vp + (int64_t)key * a.ldv + ch * 8,
+                 __builtin_amdgcn_readfirstlane(smem_lds + (uint32_t)((2 * KBUF + buf * VBUF) * 2 + (i - kDmaK) * 1024)));
+        }
+      }
+    }
+  };
   const int ntiles = (K + BK - 1) / BK;
   const int nfull = K / BK;
   f32x16_t O[QB][kNDT];
@@ -330,10 +392,29 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int dt = 0; dt < kNDT; ++dt) vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
+      for (int dt = 0; dt < kNDT; ++dt) {
+        if (kDma && dt == kNDT - 1) {
+          // (vt_frag's addressing; lanes whose columns are >= D read the constant block instead)
+          const int r = sb * 32 + 16 * s2 + 4 * hh + ((lane & 15) >> 2);
+          const int cc = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          typedef __attribute__((address_space(3))) short4_t lds_s4;
+          const uint16_t* plo = cc >= kD ? vones + ((lane & 15) >> 2) * 16 + (cc - kD) : Vb + r * kVS + cc;
+          const uint16_t* phi = cc >= kD ? plo : Vb + (r + 8) * kVS + cc;
+          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)plo);
+          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)phi);
+          vf[s2][dt] = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        } else {
+          vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
+        }
+      }
   };
 
-  stage_all(0, 0, kF16);
+  if constexpr (kDma) {
+    dma_tile(0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): Q and this wave's DMA of tile 0
+  } else {
+    stage_all(0, 0, kF16);
+  }
   __syncthreads();
 
   // ---- reference point: the row maximum of c s over the first 32 keys (F16: Q column D is still 0)
@@ -404,7 +485,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     constexpr bool kMasked = decltype(masked)::value;
     constexpr int kNcw = nchunks(role);
     const int buf = kt & 1;
-    if constexpr (kMore) stage_load(kt + 1, role);
+    if constexpr (kMore) {
+      if constexpr (kDma) dma_tile(kt + 1, buf ^ 1);   // buf ^ 1 was last read before the previous barrier
+      else stage_load(kt + 1, role);
+    }
     if constexpr (kFlagSync)
       if (kt >= 1) tsync_wait(buf, WAVES * ((kt + 1) >> 1));   // every wave's chunks of this tile
     const uint16_t* const Kb = Ks + buf * KBUF + sbo * 32 * kKS;   // (this wave's key half)
@@ -414,6 +498,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     constexpr bool kLean = (FORM & 1) != 0;
     constexpr bool kLeanK = kLean && (FORM & 4) == 0;   // FORM bit 4: LEAN V, double-buffered K
     constexpr bool kValuFirst = (FORM & 2) != 0;
+    constexpr bool kSplitTrans = (FORM & 4194304) != 0;
     short8_t kf[2][kNKT];
     short8_t vf[2][2][kNDT];
     f32x16_t S[2];
@@ -488,7 +573,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       constexpr bool kInW = x >= kWs && x < kWe;
       constexpr int c0 = kInW ? ((x - kWs) * kNcw + kWn - 1) / kWn : 0;
       constexpr int c1 = kInW ? ((x + 1 - kWs) * kNcw + kWn - 1) / kWn : 0;
-      constexpr bool kStw = kMore && c1 > c0;
+      constexpr bool kStw = kMore && c1 > c0 && !kDma;
       constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
       if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
       if constexpr (kRdKEarly) read_k(Kb, sb + 1, kf[0]);
@@ -520,6 +605,12 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
           if constexpr (kValuFirst) {
             __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
             __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
+          } else if constexpr (kSplitTrans) {
+            // FORM bit 4194304: the slot's VALU between its exponentials, so a pack rarely sits
+            // right behind the exp it reads (the trans -> VALU hazard's s_nop)
+            __builtin_amdgcn_sched_group_barrier(0x400, (te + 1) / 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
+            __builtin_amdgcn_sched_group_barrier(0x400, te - (te + 1) / 2, 0);
           } else {
             __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
@@ -569,6 +660,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
         }
       }
     }
+    if constexpr (kDma && kMore) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's DMA of tile kt + 1
     if constexpr (kFlagSync) tsync_signal(2 + buf);   // this wave's reads of buf are done
     else __syncthreads();
     stamp(3 + 2 * kt);
@@ -595,6 +687,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 #pragma unroll
         for (int r = 0; r < 16; ++r) nf = __builtin_fmaf(O[b][dt][r], 0.f, nf);   // NaN iff some O is inf/NaN
     bad |= !(nf == 0.f);
+    if constexpr (kU16Max) ovf |= kmag.x >= 0x4780 || kmag.y >= 0x4780;
     const bool any_bad = __any(bad || ovf) || (FORM & 1024) != 0;   // FORM bit 1024: always recompute
     if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
   }
@@ -768,8 +861,15 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
       case 143: return (int)launch<80, 8, 2, 128, true, 1 | 524288>(a, st);
       case 144: return (int)launch<80, 8, 2, 128, true, 1 | 128 | 524288>(a, st);   // + split staging
       case 145: return (int)launch<80, 8, 1, 128, true, 1 | 524288>(a, st);
+      // DMA staging (no staging VGPRs): alone, and with the key split over two waves per SIMD
+      case 150: return (int)launch<80, 4, 2, 128, true, 1 | 1048576>(a, st);
+      case 151: return (int)launch<80, 8, 2, 128, true, 1 | 524288 | 1048576>(a, st);
+      case 152: return (int)launch<80, 8, 2, 128, true, 1 | 8 | 524288 | 1048576>(a, st);
 #endif
-      default: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
+      // d = 80 (one wave per SIMD): the compiler's own schedule (no sched_group_barrier pinning)
+      // measured 0.0269 vs 0.0277-0.0278 ms at G2 (profiles/r04/ab_d80_r04f.log; variant 92 is the
+      // pinned schedule, round 3's default)
+      default: return (int)launch<80, 4, 2, 128, false, 1>(a, st);
     }
   }
   switch (a.variant) {
@@ -810,6 +910,11 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 140: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 262144>(a, st);
     case 141: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 16>(a, st);
     case 142: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 131072>(a, st);   // no priority duty
+    // round 4: the exponentials split around the slot's VALU (160), the packed-u16 K range check
+    // (161), both (162)
+    case 160: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304>(a, st);
+    case 161: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608>(a, st);
+    case 162: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304 | 8388608>(a, st);
 #endif
     case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
