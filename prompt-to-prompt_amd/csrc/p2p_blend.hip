@@ -140,11 +140,45 @@ __device__ __forceinline__ void build_blend_mask(const float* ws0, const float* 
       }
     }
     float* const dst = sidx == 0 ? L.mean_a[k] : L.mean_s[k];
+    float pmax = -INFINITY;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (px0 + q < R2) dst[px0 + q] = acc[q] / (float)LH;
+      if (px0 + q < R2) {
+        const float mv = acc[q] / (float)LH;
+        dst[px0 + q] = mv;
+        pmax = fmaxf(pmax, mv);
+      }
+    // the wave holds its whole plane: its maximum needs no cross-wave reduction
+    pmax = wave_max(pmax);
+    if ((tid & 63) == 0) L.red[0][g] = pmax;
   }
   __syncthreads();
+  if (lat_h >= R && lat_w >= R) {
+    // Upsampling samples every map pixel, and a 3x3 max-pool keeps the plane's maximum (every
+    // pixel lies in its own window), so the per-image maxima of the pooled / unpooled upsampled
+    // maps are the four plane maxima above -- the same floats the generic path below reduces to.
+    // Pool on the fly and threshold: one more barrier in all (mask per map pixel, gathered by the
+    // nearest upsampling: identical per output pixel, evaluated R*R times instead of H*W)
+    const float v0 = L.red[0][0], vb = L.red[0][1], s0m = L.red[0][2], sbm = L.red[0][3];
+    for (int pix = tid; pix < R2; pix += 256) {
+      const int y = pix / R, x = pix - y * R;
+      float p0 = -INFINITY, pb = -INFINITY;
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int yy = y + dy, xx = x + dx;
+          if (yy >= 0 && yy < R && xx >= 0 && xx < R) {
+            p0 = fmaxf(p0, L.mean_a[0][yy * R + xx]);
+            pb = fmaxf(pb, L.mean_a[1][yy * R + xx]);
+          }
+        }
+      bool mask = p0 / v0 > th_pool || pb / vb > th_pool;
+      if (sub) mask = mask && !(L.mean_s[0][pix] / s0m > th_sub || L.mean_s[1][pix] / sbm > th_sub);
+      L.msrc[pix] = mask ? 1.f : 0.f;
+    }
+    __syncthreads();
+    return;
+  }
+  // generic path (latent smaller than the maps: the nearest down-sampling skips map pixels)
   // 3x3 max-pool, stride 1, padding 1 (padding never wins: -inf)
   for (int i = tid; i < 2 * R2; i += 256) {
     const int k = i / R2, pix = i - k * R2;

@@ -917,10 +917,12 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 162: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304 | 8388608>(a, st);
 #endif
     case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
+    case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
-    // three of every four steps: G1 0.1867 ms vs 0.1880-0.1885 for priority on alternate step pairs
-    // (133) and 0.2056 for round 2 (profiles/r03/g1_ab/r03y_ab.log)
-    default: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);
+    // three of every four steps (round 3: 0.1867 ms vs 0.1880-0.1885 for priority on alternate step
+    // pairs and 0.2056 for round 2, profiles/r03/g1_ab/r03y_ab.log), and K's f16 range check as a
+    // packed-u16 maximum (round 4: 0.1864-0.1865 vs 0.1881-0.1889 ms, profiles/r04/ab/g1_r04h.log)
+    default: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 8388608>(a, st);
   }
 #endif
 }
