@@ -1342,11 +1342,6 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       }
     }
   };
-  auto stage = [&](int e, bool withV) {
-    Chunk8<IO> kc[NCH], vc[NCH];
-    load_kv(e, kc, vc, withV);
-    store_kv(kc, vc, withV);
-  };
   // exact softmax of S^T = K_e Q_e^T over the K keys for this lane's query row (K rows past
   // K hold stale LDS: their accumulator rows are replaced by -inf, never used)
   // kShort (K <= (KB-1)*32 + 16, e.g. the 77 text tokens): registers 8..15 of the last key block
@@ -1406,7 +1401,6 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   float sv[KB][16];
   // dense edit (bf16 PV path, program carries the f16 mapper tile): R = P0 . M_e on the MFMA
   constexpr bool kDenseOk = DENSE && MP::kElemBytes == 2;  // separate instantiation: its VGPRs
-  constexpr int kDenseTile = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * 2;  // bytes of the f16 tile
   // the dense edit's per-column blend coefficients A | B: static LDS, so the store epilogue's
   // per-wave slab (which overlays the dead mapper tile) never overlaps them
   __shared__ __attribute__((aligned(16))) float dcol[kDenseOk ? 2 * KR : 4];

@@ -28,11 +28,13 @@ def ref(q, k, v, H, qk_src=None):
     return (p @ vh).permute(0, 2, 1, 3).reshape(N, P, C)
 
 
-def check(N, P, K, d, H=8, qscale=1.0, qk_src=None, dtype=torch.bfloat16):
+def check(N, P, K, d, H=8, qscale=1.0, qk_src=None, dtype=torch.bfloat16, big_head=None):
     g = torch.Generator(device="cuda").manual_seed(P * 7 + K)
     C = H * d
     q = (qscale * torch.randn(N, P, C, device="cuda", generator=g)).to(dtype)
     k = torch.randn(N, K, C, device="cuda", generator=g).to(dtype)
+    if big_head is not None:   # one K element past the f16 range: that head's workgroups recompute exactly
+        k[:, K // 3, big_head * d] = 1e5
     v = torch.randn(N, K, C, device="cuda", generator=g).to(dtype)
     o = torch.empty_like(q)
     _hip.self_attn(q, k, v, o, H, d ** -0.5, qk_src=qk_src)
@@ -61,6 +63,11 @@ def main():
         "remap": check(8, 1024, 1024, d0, qk_src=[0, 1, 2, 3, 4, 4, 4, 4]),
         "ragged": check(2, 1000, 777, d0),
         "f32in": check(2, 2048, 2048, d0, dtype=torch.float32),
+        # an odd number of (entry, head, query tile) items and a ragged last key tile; a workgroup
+        # holding items of two heads, one of them on the exact path (chained items: re-staging)
+        "odd": check(1, 2560, 2000, d0, H=1),
+        "exact_h0": check(1, 2560, 2048, d0, H=2, big_head=0),
+        "exact_h1": check(1, 2560, 2048, d0, H=2, big_head=1),
     }
     ok = all(e < 2.0 ** -7 * 2 for e in errs.values())
     P, d = (int(x) for x in os.environ.get("G1AB_SHAPE", "4096,40").split(","))

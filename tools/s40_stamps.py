@@ -1,8 +1,8 @@
 """Where a wave of the d = 40 self-attention kernel spends its cycles (experiments build, variant
-71 = the production shape with s_memtime stamps): prologue, per-tile compute, barrier wait per
-tile, recompute check + epilogue.  Stamps come from the first 256 workgroups of a config-2 G1
+163 = the production shape with s_memtime stamps): prologue, per-tile compute, barrier wait per
+tile, recompute check + epilogue, and the launch timeline.  Stamps of the first S40_NWG (512) workgroups of a config-2 G1
 launch (N = 8, H = 8, P = K = 4096, d = 40).
-Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=71 python tools/s40_stamps.py
+Usage: P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=163 python tools/s40_stamps.py
        S40_STAMPS=P,d,waves,bk,qb (default 4096,40,8,256,2; the d = 80 stamped variant 103:
        S40_STAMPS=1024,80,4,128,2)"""
 import ctypes
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from p2p_amd import _hip  # noqa: E402
 
-SLOTS, NWG = 40, 256
+SLOTS, NWG = 40, int(os.environ.get("S40_NWG", "512"))
 P, D, WAVES, BK, QB = (int(x) for x in os.environ.get("S40_STAMPS", "4096,40,8,256,2").split(","))
 NTILES = P // BK
 X = (BK // 32) * QB   # 32x32 blocks per tile per wave
@@ -65,6 +65,18 @@ def main():
     arr = st[:, :, 2:2 + 2 * NTILES:2]
     skew = arr.max(1) - arr.min(1)
     print(f"  arrival skew per tile (max-min over the waves): median {med(skew):.0f}, p90 {float(np.percentile(skew, 90)):.0f}")
+    # launch timeline (s_memrealtime, 100 MHz): workgroup busy time against the launch span
+    rs, re_ = st[:, 0, 38], st[:, 0, 39]
+    span = (re_.max() - rs.min()) * 10.0   # ns
+    busy = float(((re_ - rs) * 10.0).sum())
+    ncu = 256
+    print(f"  timeline: span {span / 1e3:.1f} us, workgroup time summed {busy / 1e3:.1f} us over {NWG} workgroups;"
+          f" busy fraction of {ncu} CUs {busy / (ncu * span):.3f}; per-workgroup median {med((re_ - rs) * 10.0) / 1e3:.2f} us")
+    order = np.argsort(rs)
+    rel = (rs[order] - rs.min()) * 10.0 / 1e3
+    print("  start times (us) by rank: " + " ".join(f"{rel[i]:.1f}" for i in (0, 64, 128, 255, 256, 320, 384, 448, NWG - 1) if i < NWG))
+    ends = np.sort((re_ - rs.min()) * 10.0 / 1e3)
+    print("  end times (us) by rank: " + " ".join(f"{ends[i]:.1f}" for i in (0, 64, 128, 255, 256, 320, 384, 448, NWG - 1) if i < NWG))
     start_skew = t0.max(1) - t0.min(1)
     print(f"  workgroup start skew {med(start_skew):.0f}; workgroups' start spread {float(t0[:, 0].max() - t0[:, 0].min()):.0f}")
 
