@@ -156,7 +156,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   uint16_t* const Vs = smem + 2 * KBUF;
   constexpr int kOS = kD + 8;   // output row in LDS: 16-byte aligned, rows on distinct banks
   static_assert(WAVES * 32 * QB * kOS <= 2 * KBUF + 2 * VBUF, "epilogue rows fit the tile buffers");
-  __shared__ int wg_flag[2];   // per chained item
+  __shared__ int wg_flag;
   __shared__ int tsync[4];
 
   const int tid = threadIdx.x;
@@ -166,61 +166,40 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   const int qi = lane & 31;
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  int srow = logical;   // (stamp row: the item)
   auto stamp = [&](int idx) __attribute__((always_inline)) {
 #ifdef P2P_EXPERIMENTS
     if constexpr ((FORM & 16) != 0)
-      if (srow < kStampWgs && lane == 0 && idx < kStampSlots) {
-        g_s40_stamps[(srow * WAVES + wave) * kStampSlots + idx] = __builtin_amdgcn_s_memtime();
+      if (logical < kStampWgs && lane == 0 && idx < kStampSlots) {
+        g_s40_stamps[(logical * WAVES + wave) * kStampSlots + idx] = __builtin_amdgcn_s_memtime();
         if (idx == 0 || idx == 37)
-          g_s40_stamps[(srow * WAVES + wave) * kStampSlots + 38 + (idx == 37)] = __builtin_amdgcn_s_memrealtime();
+          g_s40_stamps[(logical * WAVES + wave) * kStampSlots + 38 + (idx == 37)] = __builtin_amdgcn_s_memrealtime();
       }
 #endif
   };
   stamp(0);
-  // FORM bit 33554432 (chained items): a workgroup runs IPW = 2 (entry, head, query tile) items
-  // back to back as one stream of tiles -- the last tile of an item stages the next item's first
-  // tile and loads its Q rows, so only the launch's first items pay the cold prologue, and the
-  // grid is one workgroup per CU instead of two rounds of them
-  constexpr bool kChain = (FORM & 33554432) != 0;
-  constexpr int IPW = kChain ? 2 : 1;
-  static_assert(!kChain || (!kKSplit && !kFlagSync && !kDma), "chained items: register staging, one key range");
-  const int n_items = a.n_qtiles * a.H * a.N;
   // FORM bit 8192: heads fastest -- one XCD then runs all heads of a query tile (whole q / o lines
   // in its L2) and, with xcd_remap's contiguous chunks, all tiles of one entry (its K / V once)
   int qt, h, n;
-  auto decode_to = [&](int item, int& qt_, int& h_, int& n_) __attribute__((always_inline)) {
-    if constexpr ((FORM & 8192) != 0) {
-      h_ = item % a.H;
-      qt_ = (item / a.H) % a.n_qtiles;
-      n_ = item / a.H / a.n_qtiles;
-    } else {
-      qt_ = item % a.n_qtiles;
-      h_ = (item / a.n_qtiles) % a.H;
-      n_ = item / a.n_qtiles / a.H;
-    }
-  };
-  // (chained items: workgroup l runs items l, l + grid, ... -- the same items at the same time as
-  // the one-item grid's rounds of workgroups)
-  decode_to(logical, qt, h, n);
+  if constexpr ((FORM & 8192) != 0) {
+    h = logical % a.H;
+    qt = (logical / a.H) % a.n_qtiles;
+    n = logical / a.H / a.n_qtiles;
+  } else {
+    qt = logical % a.n_qtiles;
+    h = (logical / a.n_qtiles) % a.H;
+    n = logical / a.n_qtiles / a.H;
+  }
+  const int src = a.qk_src[n];
   const int khalf = kKSplit ? __builtin_amdgcn_readfirstlane(wave) / WQ : 0;   // key half (key split)
-  const int wq = __builtin_amdgcn_readfirstlane(kKSplit ? wave - khalf * WQ : wave);
+  const int wq = kKSplit ? wave - khalf * WQ : wave;
   const int sbo = khalf * NSBW;                   // first sub-block of this wave in a tile
+  const int pw = (qt * WQ + wq) * 32 * QB;        // first query of this wave
   const int K = a.K;
   const float c = a.scale_log2;
 
-  // the item's first query of this wave and its q / k / v bases (re-bound per chained item)
-  int pw;
-  const uint16_t *qp, *kp, *vp;
-  auto bind_to = [&](int qt_, int h_, int n_, int& pw_, const uint16_t*& qp_, const uint16_t*& kp_,
-                     const uint16_t*& vp_) __attribute__((always_inline)) {
-    const int src = a.qk_src[n_];
-    pw_ = (qt_ * WQ + wq) * 32 * QB;
-    qp_ = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h_ * kD;
-    kp_ = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h_ * kD;
-    vp_ = static_cast<const uint16_t*>(a.v) + (int64_t)n_ * a.bsv + h_ * kD;
-  };
-  bind_to(qt, h, n, pw, qp, kp, vp);
+  const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * kD;
+  const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * kD;
+  const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * kD;
 
   // padding columns (written once; staging writes columns 0..D-1 only): F16 K column D = f16 1.0
   // (the -m column), D+1..DK-1 = 0; V column D = bf16 1.0 (row sums), D+1..DV-1 = 0
@@ -236,7 +215,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   }
   if constexpr (kDma)
     if (tid < 64) vones[tid] = (tid & 15) == 0 ? (uint16_t)0x3F80 : (uint16_t)0;   // [4][16]: column 0 = 1
-  if (tid < IPW) wg_flag[tid] = 0;
+  if (tid == 0) wg_flag = 0;
   if constexpr (kFlagSync)
     if (tid < 4) tsync[tid] = 0;
 
@@ -251,40 +230,27 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   u16x2_t kmag = {0, 0};
   short8_t qf[QB][kNKT];
-  // raw bf16 rows of the item at (qpx, pwx) into qf; then, F16 form, prescaled by c and rounded
-  // to f16 in place (chained items: the raw loads are issued inside the previous item's last tile)
-  auto load_q_raw = [&](const uint16_t* qpx, int pwx) __attribute__((always_inline)) {
+  auto load_q = [&](bool prescale) __attribute__((always_inline)) {
 #pragma unroll
     for (int b = 0; b < QB; ++b)
 #pragma unroll
       for (int t = 0; t < kNKT; ++t) {
         const int col = 16 * t + 8 * hh;
-        const int p = pwx + 32 * b + qi;
+        const int p = pw + 32 * b + qi;
         short8_t v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
-        if (p < a.P && col < kD) v = *reinterpret_cast<const short8_t*>(qpx + (int64_t)p * a.ldq + col);
-        qf[b][t] = v;
-      }
-  };
-  auto prescale_q = [&]() __attribute__((always_inline)) {
+        if (p < a.P && col < kD) v = *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + col);
+        if (prescale) {
+          float mx = 0.f;
 #pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-      for (int t = 0; t < kNKT; ++t) {
-        short8_t v = qf[b][t];
-        float mx = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = bf2f((uint16_t)v[j]) * c;
-          mx = fmaxf(mx, fabsf(x));
-          v[j] = (short)__builtin_bit_cast(uint16_t, (_Float16)x);
+          for (int j = 0; j < 8; ++j) {
+            const float x = bf2f((uint16_t)v[j]) * c;
+            mx = fmaxf(mx, fabsf(x));
+            v[j] = (short)__builtin_bit_cast(uint16_t, (_Float16)x);
+          }
+          ovf |= !(mx < 65520.f);
         }
-        ovf |= !(mx < 65520.f);
         qf[b][t] = v;
       }
-  };
-  auto load_q = [&](bool prescale) __attribute__((always_inline)) {
-    load_q_raw(qp, pw);
-    if (prescale) prescale_q();
   };
   load_q(kF16);
   // F16: Q column D (k step D/16, lane half (D%16)/8, element D%8) holds -m
@@ -304,20 +270,16 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   short8_t kreg[CMAX], vreg[NCH];
   uint32_t koff[CMAX], voff[NCH];
   int lrow[CMAX], lch[CMAX];
-  // (computed again by the exact recompute, so these registers die with the last fast tile)
-  auto chunk_geom = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < CMAX; ++i) {
-      const int cidx = stid + i * sstride;
-      const int row = min(cidx / kCPR, BK - 1);
-      const int ch = cidx - (cidx / kCPR) * kCPR;
-      lrow[i] = row;
-      lch[i] = ch;
-      koff[i] = (uint32_t)((row * (int)(kSplit && vrole ? a.ldv : a.ldk) + ch * 8) * 2);
-      if (i < NCH) voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
-    }
-  };
-  chunk_geom();
+  for (int i = 0; i < CMAX; ++i) {
+    const int cidx = stid + i * sstride;
+    const int row = min(cidx / kCPR, BK - 1);
+    const int ch = cidx - (cidx / kCPR) * kCPR;
+    lrow[i] = row;
+    lch[i] = ch;
+    koff[i] = (uint32_t)((row * (int)(kSplit && vrole ? a.ldv : a.ldk) + ch * 8) * 2);
+    if (i < NCH) voff[i] = (uint32_t)((row * (int)a.ldv + ch * 8) * 2);
+  }
   const int64_t kbytes = ((int64_t)(K - 1) * a.ldk + kD) * 2;
   const int64_t vbytes = ((int64_t)(K - 1) * a.ldv + kD) * 2;
   const int64_t kstep = (int64_t)BK * a.ldk * 2;
@@ -326,11 +288,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     constexpr int sn = decltype(role)::value == 0 ? NT : NT / 2;
     return (BK * kCPR) % sn == 0 || stid + i * sn < BK * kCPR;
   };
-  // tile kt of the item whose k / v bases are (kpx, vpx) into this thread's staging registers
-  auto stage_load_from = [&](const uint16_t* kpx, const uint16_t* vpx, int kt, auto role) __attribute__((always_inline)) {
+  auto stage_load = [&](int kt, auto role) __attribute__((always_inline)) {
     constexpr int kRole = decltype(role)::value;
-    const __amdgpu_buffer_rsrc_t rk = make_rsrc(reinterpret_cast<const char*>(kpx) + kt * kstep, kbytes - kt * kstep);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(reinterpret_cast<const char*>(vpx) + kt * vstep, vbytes - kt * vstep);
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(reinterpret_cast<const char*>(kp) + kt * kstep, kbytes - kt * kstep);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(reinterpret_cast<const char*>(vp) + kt * vstep, vbytes - kt * vstep);
 #pragma unroll
     for (int i = 0; i < nchunks(role); ++i)
       if (chunk_live(i, role)) {
@@ -339,7 +300,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
           vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (int)voff[i], 0, 0));
       }
   };
-  auto stage_load = [&](int kt, auto role) __attribute__((always_inline)) { stage_load_from(kp, vp, kt, role); };
   // chunk i into LDS buffer buf: K as f16 (fast form; exact for magnitudes in [2^-14, 65504] --
   // smaller ones become f16 subnormals, absolute error < 2^-25 --, RTZ packing would clamp past
   // 65504 silently, so the range is checked) or raw bf16 (exact path)
@@ -422,22 +382,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   };
   const int ntiles = (K + BK - 1) / BK;
   const int nfull = K / BK;
-  // chained items: the LDS buffer of the item's first tile, and whether the item stages its own
-  // first tile (after an exact recompute)
-  int tpar = 0;
-  bool restage = false;
-  // (compile-time item index: one copy of the body per item, so the straight-line single-item
-  // kernel is unchanged -- a runtime loop around it, even of one trip, cost 30 spilled registers)
-  static_for<IPW>([&](auto itc) __attribute__((always_inline)) {
-  constexpr int it = decltype(itc)::value;
-  const int item = logical + it * (int)gridDim.x;
-  if (it > 0 && item >= n_items) return;
-  if constexpr (it > 0) {
-    srow = item;
-    stamp(0);
-  }
-  const int next_item = item + (int)gridDim.x;
-  const bool has_next = kChain && it + 1 < IPW && next_item < n_items;
   f32x16_t O[QB][kNDT];
   float m_ref[QB];
 #pragma unroll
@@ -471,27 +415,18 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       }
   };
 
-  if constexpr (it == 0) {
-    if constexpr (kDma) {
-      dma_tile(0, 0);
-      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): Q and this wave's DMA of tile 0
-    } else {
-      stage_all(0, 0, kF16);
-    }
-    __syncthreads();
-  } else if (restage) {
-    load_q(kF16);
-    stage_all(0, tpar, kF16);
-    __syncthreads();
+  if constexpr (kDma) {
+    dma_tile(0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): Q and this wave's DMA of tile 0
   } else {
-    // Q's rows and the first tile were loaded by the previous item's last tile
-    if constexpr (kF16) prescale_q();
+    stage_all(0, 0, kF16);
   }
+  __syncthreads();
 
   // ---- reference point: the row maximum of c s over the first 32 keys (F16: Q column D is still 0)
   {
     short8_t kf[kNKT];
-    read_k(Ks + tpar * KBUF, 0, kf);
+    read_k(Ks, 0, kf);
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       f32x16_t acc = f32x16_t{};
@@ -551,25 +486,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // ---- one tile of the fast form, software-pipelined over its X blocks.  more: the next tile
   // is staged during this one (compile-time, so the tile body is one basic block); masked: keys
   // past K in this tile
-  // chain (chained items, the item's last tile): the tile staged is the next item's first, and
-  // the next item's Q rows load once this tile's last Q K^T has read qf
-  auto tile = [&](int kt, auto more, auto masked, auto role, auto chain) __attribute__((always_inline)) {
+  auto tile = [&](int kt, auto more, auto masked, auto role) __attribute__((always_inline)) {
     constexpr bool kMore = decltype(more)::value;
     constexpr bool kMasked = decltype(masked)::value;
-    constexpr bool kChainT = decltype(chain)::value;
-    static_assert(!kChainT || kMore, "a chained tile stages the next item's first tile");
     constexpr int kNcw = nchunks(role);
-    const int buf = (kt + tpar) & 1;
-    int pwn = 0;
-    const uint16_t *qpn = nullptr, *kpn = nullptr, *vpn = nullptr;
-    if constexpr (kChainT) {
-      int qt2, h2, n2;
-      decode_to(next_item, qt2, h2, n2);
-      bind_to(qt2, h2, n2, pwn, qpn, kpn, vpn);
-    }
+    const int buf = kt & 1;
     if constexpr (kMore) {
       if constexpr (kDma) dma_tile(kt + 1, buf ^ 1);   // buf ^ 1 was last read before the previous barrier
-      else if constexpr (kChainT) stage_load_from(kpn, vpn, 0, role);
       else stage_load(kt + 1, role);
     }
     if constexpr (kFlagSync)
@@ -611,10 +534,12 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       float e[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float s = kF16 ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
+        // (FORM bits 67108864 / 134217728: timing probes of the experiments build -- no scale-and-
+        // shift fma / no exponential; the results are wrong)
+        float s = (kF16 || (FORM & 67108864) != 0) ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
         if constexpr (kMasked)
           if (kt * BK + (sbo + sb) * 32 + acc_row(r, hh) >= K) s = -INFINITY;
-        e[r] = fast_exp2(s);
+        e[r] = (FORM & 134217728) != 0 ? s : fast_exp2(s);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -658,7 +583,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       constexpr int c1 = kInW ? ((x + 1 - kWs) * kNcw + kWn - 1) / kWn : 0;
       constexpr bool kStw = kMore && c1 > c0 && !kDma;
       constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
-      if constexpr (kChainT && x == X - 1) load_q_raw(qpn, pwn);   // qf's last reader was step X - 2
       if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
       if constexpr (kRdKEarly) read_k(Kb, sb + 1, kf[0]);
       if constexpr (!kLean && kRdV) read_v(Vb, sb + 1, vf[(sb + 1) & 1]);
@@ -752,16 +676,9 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr std::false_type kNo{};
   constexpr std::true_type kYes{};
   auto run_tiles = [&](auto role) __attribute__((always_inline)) {
-    for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, kYes, kNo, role, kNo);
-    if constexpr (kChain) {
-      if (has_next) {
-        if (nfull == ntiles) tile(ntiles - 1, kYes, kNo, role, kYes);
-        else tile(ntiles - 1, kYes, kYes, role, kYes);
-        return;
-      }
-    }
-    if (nfull == ntiles) tile(ntiles - 1, kNo, kNo, role, kNo);
-    else tile(ntiles - 1, kNo, kYes, role, kNo);
+    for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, kYes, kNo, role);
+    if (nfull == ntiles) tile(ntiles - 1, kNo, kNo, role);
+    else tile(ntiles - 1, kNo, kYes, role);
   };
   if constexpr (!kSplit) run_tiles(std::integral_constant<int, 0>{});
   else if (vrole) run_tiles(std::integral_constant<int, 2>{});
@@ -780,15 +697,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     bad |= !(nf == 0.f);
     if constexpr (kU16Max) ovf |= kmag.x >= 0x4780 || kmag.y >= 0x4780;
     const bool any_bad = __any(bad || ovf) || (FORM & 1024) != 0;   // FORM bit 1024: always recompute
-    if (lane == 0 && any_bad) atomicOr(&wg_flag[it], 1);
+    if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
   }
   __syncthreads();
-  restage = wg_flag[it] != 0;   // (the recompute reuses buffer 0 and qf)
-  if (__builtin_expect(wg_flag[it] != 0, 0)) {
+  if (__builtin_expect(wg_flag != 0, 0)) {
     // ---- exact recompute: bf16 Q and K as they are, S = Q K^T in f32, running max per
     // 32-key sub-block with the defer-max rule (the sub-block's P V follows at once)
     load_q(false);
-    chunk_geom();
     float m_run[QB];
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
@@ -876,11 +791,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // are dead: every wave has passed the last tile's barrier) and stores them back as contiguous
   // 16-byte chunks, consecutive lanes along a row
   if (kKSplit && khalf != 0) return;   // (key split: the first half holds the combined rows)
-  // (chained items: the V image of the buffer the last tile read -- the other one holds the next
-  // item's first tile)
-  const int lbuf = (ntiles - 1 + tpar) & 1;
-  static_assert(!kChain || WAVES * 32 * QB * kOS <= VBUF, "chained epilogue rows fit one V image");
-  uint16_t* const orow = (kChain ? Vs + lbuf * VBUF : smem) + wq * (32 * QB * kOS);
+  uint16_t* const orow = smem + wq * (32 * QB * kOS);
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const float l = __shfl(O[b][kLdt][kLr], lane & 31);
@@ -912,27 +823,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     }
   }
   stamp(37);
-  if constexpr (kChain) {
-    if (has_next) {
-      // the V rows this wave's output overlaid get their padding columns back (row-sum column
-      // D = 1, then 0), and no wave stages into this buffer before every wave is done with it
-      constexpr int kRows = (32 * QB * kOS + kVS - 1) / kVS;
-      constexpr int kPc = (kDV - kD) / 8;
-      uint16_t* const vrows = Vs + lbuf * VBUF + wq * (32 * QB * kOS) / kVS * kVS;
-      static_assert((32 * QB * kOS) % kVS == 0, "a wave's output rows cover whole V rows");
-#pragma unroll
-      for (int j = lane; j < kRows * kPc; j += 64) {
-        const int r = j / kPc, cc = j - (j / kPc) * kPc;
-        *reinterpret_cast<short8_t*>(vrows + r * kVS + kD + 8 * cc) =
-            short8_t{(short)(cc == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
-      }
-      __syncthreads();
-      tpar = (tpar + ntiles) & 1;
-      decode_to(next_item, qt, h, n);
-      bind_to(qt, h, n, pw, qp, kp, vp);
-    }
-  }
-  });   // items
 }
 
 template <int D, int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
@@ -940,8 +830,7 @@ hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   constexpr int WQ = (FORM & 524288) != 0 ? WAVES / 2 : WAVES;   // query waves (key split: half)
   b.n_qtiles = (a.P + 32 * QB * WQ - 1) / (32 * QB * WQ);
-  constexpr int IPW = (FORM & 33554432) != 0 ? 2 : 1;   // items per workgroup (chained items)
-  dim3 grid((b.n_qtiles * a.H * a.N + IPW - 1) / IPW), block(64 * WAVES);
+  dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
   hipLaunchKernelGGL((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
 }
@@ -976,6 +865,11 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
       case 102: return (int)launch<80, 8, 1, 128, true, 1>(a, st);
       case 103: return (int)launch<80, 4, 2, 128, true, 1 | 16>(a, st);   // 92 with clock stamps
       case 164: return (int)launch<80, 4, 2, 128, false, 1 | 16>(a, st);  // default with clock stamps
+      // timing probes (wrong results): no scale-and-shift fma, no exponential, neither
+      // (profiles/r04/d80_probes_r04m.log: 29.2 / 29.2 / 28.6 / 27.2 us -- not VALU-bound)
+      case 170: return (int)launch<80, 4, 2, 128, false, 1 | 67108864>(a, st);
+      case 171: return (int)launch<80, 4, 2, 128, false, 1 | 134217728>(a, st);
+      case 172: return (int)launch<80, 4, 2, 128, false, 1 | 67108864 | 134217728>(a, st);
       case 128: return (int)launch<80, 4, 2, 128, true, 1 | 8192>(a, st);  // default, heads fastest
       // key split: 8 waves, wave w and w + 4 on the two key halves of each tile (two waves per SIMD)
       case 143: return (int)launch<80, 8, 2, 128, true, 1 | 524288>(a, st);
@@ -1036,9 +930,9 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 161: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608>(a, st);
     case 162: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304 | 8388608>(a, st);
     case 163: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 16>(a, st);   // default with clock stamps
-    // chained items: two items per workgroup, one workgroup per CU (165 with clock stamps)
-    case 165: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 33554432>(a, st);
-    case 166: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 33554432 | 16>(a, st);
+    // (165/166, round 4: two chained items per workgroup -- the next item's first tile and Q rows
+    // loaded in the item's last tile -- measured 1.5-2.6 % slower, profiles/r04/chain/; code in
+    // commit 5a2e317)
 #endif
     case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
     case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
