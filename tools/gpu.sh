@@ -52,7 +52,8 @@ for step in "$@"; do
       grep '^{' "$out/prof.log" | tail -1 | tee "$out/bench_under_rocprof.json"
       find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
       db=$(find "$out/prof" -name "*.db" | head -1)
-      if [ -n "$db" ]; then python3 tools/rocpd_summary.py "$db" > "$out/rocprof_summary.txt"; sed -n '/hot path/,$p' "$out/rocprof_summary.txt" | head -14; fi ;;
+      if [ -n "$db" ]; then python3 tools/rocpd_summary.py "$db" > "$out/rocprof_summary.txt"; sed -n '/hot path/,$p' "$out/rocprof_summary.txt" | head -14; fi
+      rm -rf "$out/prof" ;;   # (the trace database of a 20-group run is far past gpurun's 64 MiB return cap)
     pmc)
       name=${arg%%:*}; counters=${arg#*:}
       run 120 "$out/pmc_$name.log" timeout -s KILL 100 rocprofv3 --pmc ${counters//,/ } --output-format csv -d "$out/pmc_$name" -o run -- python3 -u tools/g1_only.py
