@@ -1095,16 +1095,29 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.N), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v),
                "s"(a.o), "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv),
                "s"(a.bso), "s"(a.scale_log2));
-  // heads fastest (whole q / o lines per XCD, as in cross_group_kernel)
+  // Launches of one round of workgroups (<= 512: G2-G6, every workgroup resident at once):
+  // entries fastest, then heads -- xcd_remap keeps consecutive ids on one XCD, so the source's Q
+  // rows that a tile's three edit workgroups re-read (for P0) and the tile's q / o lines stay in
+  // that XCD's L2 (in the pipeline, rocprof: G2/G6 21.4 -> 20.1 us, d = 160 21.7 -> 20.9 us;
+  // profiles/r04/cross_order_r04p/).  Larger launches: heads fastest, then query tiles, edits
+  // dispatched first (whole q / o lines per XCD, as in cross_group_kernel)
   int qt, h, rest;
 #ifdef P2P_EXPERIMENTS
-  if (a.variant == 126) {   // A/B: query tiles fastest (the previous order)
+  if (a.variant == 126) {   // A/B: query tiles fastest (round 2's order)
     qt = logical % a.n_qtiles;
     h = (logical / a.n_qtiles) % a.H;
     rest = logical / a.n_qtiles / a.H;
+  } else if (a.variant == 138) {   // A/B: heads fastest at every size (round 3's order)
+    h = logical % a.H;
+    qt = (logical / a.H) % a.n_qtiles;
+    rest = logical / a.H / a.n_qtiles;
   } else
 #endif
-  {
+  if (gridDim.x <= 512) {
+    rest = logical % a.N;
+    h = (logical / a.N) % a.H;
+    qt = logical / a.N / a.H;
+  } else {
     h = logical % a.H;
     qt = (logical / a.H) % a.n_qtiles;
     rest = logical / a.H / a.n_qtiles;

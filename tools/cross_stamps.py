@@ -57,7 +57,9 @@ def run(name, P, d, store, blend):
     nq = (P + 127) // 128
     nwg = nq * H * N
     s = s[:nwg]
-    ent = N - 1 - np.arange(nwg) // (nq * H)      # heads fastest, then query tiles
+    # the kernel's work order: entries fastest for launches of <= 512 workgroups, else heads
+    # fastest, then query tiles (edits first either way)
+    ent = N - 1 - (np.arange(nwg) % N if nwg <= 512 else np.arange(nwg) // (nq * H))
     t0 = s[:, :, 0]
     print(f"== {name}: P={P} d={d} store={store} blend={blend}: {nwg} workgroups")
     plain = ent < B + 1 if not store else ent < B
