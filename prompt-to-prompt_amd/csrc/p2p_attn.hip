@@ -1284,10 +1284,31 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     if (!(tid < K || (tid < 2 * K && tsub != nullptr))) bw0 = 0.f;
     if (!(i1 < K || (i1 < 2 * K && tsub != nullptr))) bw1 = 0.f;
   }
-  // once the prologue's loads are issued: the blend weights into LDS, and this wave's rows of the
-  // running sum touched into this XCD's L2 (32 x K f32, contiguous; two loads per lane cover 32
+  // once the prologue's loads are issued: the blend weights into LDS; this wave's rows of the
+  // running sum are touched into this XCD's L2 (32 x K f32, contiguous; two loads per lane cover 32
   // rows of up to 96 keys) so the store epilogue's read-add-write finds them there.  The touches
-  // go last: they miss to HBM, and a wait for any load issued after them would wait for them too
+  // go after every other load: they miss to HBM, and a wait for any load issued after them would
+  // wait for them too
+  // The touches are issued after the workgroup's first barrier, not with the prologue: the whole
+  // launch issues its prologue loads at once, and 10 MB of touches (G2/G6) in that burst delayed
+  // every workgroup's first round trip (in the pipeline, rocprof: G2/G6 20.0 -> 19.1 us, d = 160
+  // 20.7 -> 20.4; no touches at all: 19.8 / 20.6; profiles/r04/cross_touch_r04r/).  Experiments:
+  // variant 147 = with the prologue (before), 148 = never
+  int touch_when = 1;   // 0: with the prologue, 1: after the first barrier, 2: never
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 147) touch_when = 0;
+  if (a.variant == 148) touch_when = 2;
+#endif
+  auto touch = [&]() __attribute__((always_inline)) {
+    if (stored && a.store_accumulate) {
+      const int rows = min(32, a.P - p0w);
+      const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
+      const int lines = (rows * K * 4 + 127) / 128;
+      static_assert(32 * P2P_MAX_KEYS_CROSS * 4 / 128 <= 128, "two touches per lane");
+      if (lane < lines) touch0 = g[lane * 32];
+      if (lane + 64 < lines) touch1 = g[(lane + 64) * 32];
+    }
+  };
   auto finish_prologue = [&]() __attribute__((always_inline)) {
     if (blend_on) {
       const int i1 = tid + NT;
@@ -1297,14 +1318,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       for (int i = tid; i < 2 * (P2P_MAX_KEYS_CROSS - K); i += NT)
         btab[i / (P2P_MAX_KEYS_CROSS - K)][K + i % (P2P_MAX_KEYS_CROSS - K)] = 0.f;
     }
-    if (stored && a.store_accumulate) {
-      const int rows = min(32, a.P - p0w);
-      const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
-      const int lines = (rows * K * 4 + 127) / 128;
-      static_assert(32 * P2P_MAX_KEYS_CROSS * 4 / 128 <= 128, "two touches per lane");
-      if (lane < lines) touch0 = g[lane * 32];
-      if (lane + 64 < lines) touch1 = g[(lane + 64) * 32];
-    }
+    if (touch_when == 0) touch();
   };
 
   // padding the MFMAs read but the staging never writes (disjoint from it: no extra barrier):
@@ -1480,6 +1494,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     }
     store_kv(kc0, vc0, false);
     __syncthreads();
+    if (touch_when == 1) touch();
     P2P_CROSS_STAMP(8)
     {
       // which blend halves the row uses (every wave scans the coefficients itself): bit 0 some
@@ -1540,6 +1555,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       store_kv(kc, vc, false);
     }
     __syncthreads();
+    if (touch_when == 1) touch();
     probs(qf, sv);
     load_q(n, qf);
 #pragma unroll
@@ -1566,6 +1582,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     stage_own();
   }
   __syncthreads();
+  if (!edit && touch_when == 1) touch();
   P2P_CROSS_STAMP(11)
   if (!dense || (dense_flags & 1)) {
     probs(qf, sv);
