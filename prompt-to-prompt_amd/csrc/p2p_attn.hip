@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     qt = logical % a.n_qtiles;
     h = (logical / a.n_qtiles) % a.H;
     rest = logical / a.n_qtiles / a.H;
-  } else if (a.variant == 138) {   // A/B: heads fastest at every size (round 3's order)
+  } else if (a.variant == 149) {   // A/B: heads fastest at every size (round 3's order)
     h = logical % a.H;
     qt = (logical / a.H) % a.n_qtiles;
     rest = logical / a.H / a.n_qtiles;
@@ -1294,13 +1294,32 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // every workgroup's first round trip (in the pipeline, rocprof: G2/G6 20.0 -> 19.1 us, d = 160
   // 20.7 -> 20.4; no touches at all: 19.8 / 20.6; profiles/r04/cross_touch_r04r/).  Experiments:
   // variant 147 = with the prologue (before), 148 = never
-  int touch_when = 1;   // 0: with the prologue, 1: after the first barrier, 2: never
+  // Mode 3 goes further: after the first barrier the wave reads its rows of the running sum (and
+  // its LocalBlend word-sum entries) into registers, so the store epilogue only adds and writes.
+  // (bf16 inputs only: the f32-input instantiations have no registers to spare for the rows)
+  int touch_when = std::is_same<IO, uint16_t>::value ? 3 : 1;   // 0: touches with the prologue,
+                        // 1: touches after the first barrier, 2: never, 3: the values themselves
 #ifdef P2P_EXPERIMENTS
   if (a.variant == 147) touch_when = 0;
   if (a.variant == 148) touch_when = 2;
+  if (a.variant == 156) touch_when = 1;
 #endif
+  constexpr int kRmwF4 = 32 * KR / 4;
+  f32x4_t rmwbuf[(kRmwF4 + 63) / 64];
+  float bsum_old = 0.f;
+  const int srows = min(32, a.P - p0w);
+  float* const sg = stored ? a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K : nullptr;
+  const bool rmw_vec = stored && srows > 0 && ((uintptr_t)sg & 15) == 0 && ((srows * K) & 3) == 0;
+  float* const bdst = blend_on ? a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P +
+                                     p0w + qi
+                               : nullptr;
   auto touch = [&]() __attribute__((always_inline)) {
-    if (stored && a.store_accumulate) {
+    if (touch_when == 3) {
+      if (stored && a.store_accumulate) {
+        if (rmw_vec) rmw_load<kRmwF4>(sg, srows * K, lane, rmwbuf);
+        if (blend_on && qi < srows) bsum_old = *bdst;
+      }
+    } else if (stored && a.store_accumulate) {
       const int rows = min(32, a.P - p0w);
       const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int lines = (rows * K * 4 + 127) / 128;
@@ -1494,7 +1513,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     }
     store_kv(kc0, vc0, false);
     __syncthreads();
-    if (touch_when == 1) touch();
+    if (touch_when == 1 || touch_when == 3) touch();
     P2P_CROSS_STAMP(8)
     {
       // which blend halves the row uses (every wave scans the coefficients itself): bit 0 some
@@ -1555,7 +1574,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       store_kv(kc, vc, false);
     }
     __syncthreads();
-    if (touch_when == 1) touch();
+    if (touch_when == 1 || touch_when == 3) touch();
     probs(qf, sv);
     load_q(n, qf);
 #pragma unroll
@@ -1582,7 +1601,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     stage_own();
   }
   __syncthreads();
-  if (!edit && touch_when == 1) touch();
+  if (!edit && (touch_when == 1 || touch_when == 3)) touch();
   P2P_CROSS_STAMP(11)
   if (!dense || (dense_flags & 1)) {
     probs(qf, sv);
@@ -1699,15 +1718,16 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       ss += other_half(ss);
       if (qi < rows) {
         const float acc = hh == 0 ? sa : (has_sub ? ss : 0.f);
-        float* dst = a.grp_bsum[gi] + ((int64_t)(b * 2 + hh) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w + qi;
-        *dst = a.store_accumulate ? *dst + acc : acc;
+        *bdst = a.store_accumulate ? (touch_when == 3 ? bsum_old : *bdst) + acc : acc;
       }
     }
     P2P_CROSS_STAMP(18)
     if (rows > 0) {
       float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
       const int count = rows * K;
-      if (((uintptr_t)g & 15) == 0 && (count & 3) == 0) {
+      if (touch_when == 3 && rmw_vec && a.store_accumulate) {
+        rmw_add_store<kRmwF4>(g, slab, count, lane, rmwbuf);
+      } else if (((uintptr_t)g & 15) == 0 && (count & 3) == 0) {
         store_rows_rmw<32 * KR / 4>(g, slab, count, a.store_accumulate != 0, lane);
         // keeps the prefetch touches alive (never true: a running sum of probabilities is finite)
         if (__builtin_expect(touch0 == -INFINITY || touch1 == -INFINITY, 0)) g[0] = touch0 + touch1;

@@ -291,6 +291,33 @@ __device__ __forceinline__ void store4(uint16_t* dst, float a, float b, float c,
 // Every running-sum read is issued first -- range-checked buffer loads (zeros past cnt), no
 // branch, so they all fly together -- and only then the (masked) stores: ONE memory round trip.
 // (Reads issued after stores would also wait for the stores: CDNA4's vmcnt counts both in order.)
+// The same read-add-write in two halves, for a caller that issues the reads early (their values
+// ride in registers until the slab is ready): rmw_load, then rmw_add_store.
+template <int MAXF4>
+__device__ __forceinline__ void rmw_load(const float* g, int cnt, int lane, f32x4_t (&buf)[(MAXF4 + 63) / 64]) {
+  constexpr int IT = (MAXF4 + 63) / 64;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(g, (int64_t)cnt * 4);
+#pragma unroll
+  for (int j = 0; j < IT; ++j)
+    buf[j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * j) * 16, 0, 0));
+}
+template <int MAXF4>
+__device__ __forceinline__ void rmw_add_store(float* g, const float* slab, int cnt, int lane,
+                                              f32x4_t (&buf)[(MAXF4 + 63) / 64]) {
+  constexpr int IT = (MAXF4 + 63) / 64;
+  const int n4 = cnt / 4;
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int i = lane + 64 * j;
+    buf[j] += reinterpret_cast<const f32x4_t*>(slab)[i < n4 ? i : n4 - 1];
+  }
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int i = lane + 64 * j;
+    if (i < n4) reinterpret_cast<f32x4_t*>(g)[i] = buf[j];
+  }
+}
+
 template <int MAXF4>
 __device__ __forceinline__ void store_rows_rmw(float* g, const float* slab, int cnt, bool accumulate, int lane) {
   constexpr int IT = (MAXF4 + 63) / 64;   // float4s per lane
