@@ -1497,11 +1497,13 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       load_q(n, qf1);
     }
     finish_prologue();
+    P2P_CROSS_STAMP(19)
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const int i = tid + j * NT;
       if (i < kMCh) reinterpret_cast<short8_t*>(Ms)[i] = mreg[j];
     }
+    P2P_CROSS_STAMP(20)
     {  // per-column coefficients next to the tile, read back after the barriers:
       // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B
       float* col = dcol;
@@ -1511,7 +1513,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
         col[KR + w] = ap;
       }
     }
+    P2P_CROSS_STAMP(21)
     store_kv(kc0, vc0, false);
+    P2P_CROSS_STAMP(22)
     __syncthreads();
     if (touch_when == 1 || touch_when == 3) touch();
     P2P_CROSS_STAMP(8)

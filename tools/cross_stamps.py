@@ -20,7 +20,8 @@ from p2p_amd.tokenizer import default_tokenizer  # noqa: E402
 NWG, W, SLOTS = 4096, 4, 24
 PLAIN = [(0, 1, "loads issued"), (1, 2, "LDS staged + barrier"), (2, 3, "QK + softmax"), (3, 4, "PV"),
          (4, 5, "O store")]
-EDIT = [(0, 8, "src stage + barrier"), (8, 9, "P0"), (9, 10, "R = P0 M + barrier"), (10, 11, "own stage + barrier"),
+EDIT = [(0, 19, "  (dense) loads issued"), (19, 20, "  (dense) mapper landed"), (20, 21, "  (dense) coeffs"),
+        (21, 22, "  (dense) K_src landed"), (22, 8, "  (dense) barrier"), (0, 8, "src stage + barrier"), (8, 9, "P0"), (9, 10, "R = P0 M + barrier"), (10, 11, "own stage + barrier"),
         (11, 12, "own QK + softmax"), (12, 13, "blend"), (13, 14, "store epilogue"), (14, 15, "PV"),
         (13, 16, "  store: sync + slab write"), (16, 17, "  store: sync"), (17, 18, "  store: blend sums"),
         (18, 14, "  store: read-add-write")]
