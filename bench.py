@@ -34,6 +34,54 @@ MFMA_PEAK_F32_TFLOPS = 157.3
 HBM_PEAK_GBPS = 8000.0          # spec, MI355X_MICROARCH.md:36 (6.29 TB/s measured copy)
 
 
+class FenceFreeEvent:
+    """A HIP event created with hipEventDisableSystemFence, recorded on torch's current stream.
+    torch.cuda.Event records with a system-scope release: an L2 writeback + invalidate at every
+    record, which the next kernel pays as a cold cache -- hip_runtime_api.h documents the flag as
+    the timing-only event that avoids "the cost of cache writeback and invalidation, and the
+    performance impact of those actions on the execution of following work".  The timer reads
+    the events only after torch.cuda.synchronize(), so the fence is not needed for correctness.
+    Same record()/elapsed_time() surface as torch.cuda.Event; torch's own HIP runtime (already
+    loaded: libamdhip64.so.7) creates and records them."""
+    _hip = None
+
+    @classmethod
+    def _lib(cls):
+        if cls._hip is None:
+            import ctypes
+            L = ctypes.CDLL("libamdhip64.so.7")
+            L.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            L.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            cls._hip = L
+        return cls._hip
+
+    def __init__(self):
+        import ctypes
+        self._ctypes = ctypes
+        self.ev = ctypes.c_void_p()
+        rc = self._lib().hipEventCreateWithFlags(ctypes.byref(self.ev), 0x20000000)   # hipEventDisableSystemFence
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
+
+    def record(self):
+        rc = self._lib().hipEventRecord(self.ev, ctypes_stream())
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed: {rc}")
+
+    def elapsed_time(self, end) -> float:
+        ms = self._ctypes.c_float()
+        rc = self._lib().hipEventElapsedTime(self._ctypes.byref(ms), self.ev, end.ev)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
+        return ms.value
+
+
+def ctypes_stream():
+    import ctypes
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
 class LaunchTimer:
     """HIP events around the launches of interest, on the launch stream (torch's current stream,
     which the binding launches on):
@@ -46,8 +94,9 @@ class LaunchTimer:
     Every record also carries the index of the batch (edit group) it ran in, so per-batch
     averages show clock droop over a long run."""
 
-    def __init__(self, n_query=4096):
+    def __init__(self, n_query=4096, fence_free=True):
         self.n_query = n_query
+        self.event = FenceFreeEvent if fence_free else (lambda: torch.cuda.Event(enable_timing=True))
         self.rec = {}            # name -> list of (start event, end event, work, batch)
         self._pending = None     # (start event, [(name, work), ...])
         self.enabled = False
@@ -78,7 +127,7 @@ class LaunchTimer:
         if not self.enabled:
             return
         info = info or {"stored": 0, "accumulate": False}
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = self.event()
         ev.record()
         self._pending = (ev, self._names(kind, t, info))
         if kind == "cross" and "n_groups" in info:
@@ -86,7 +135,7 @@ class LaunchTimer:
 
     def after(self, kind, t, info=None):
         if self._pending is not None:
-            ev = torch.cuda.Event(enable_timing=True)
+            ev = self.event()
             ev.record()
             start, names = self._pending
             for name, work in names:
@@ -96,7 +145,7 @@ class LaunchTimer:
     def before_aux(self, name, nbytes):
         """The LocalBlend mask and latent-step launches (HBM-type helpers), with their bytes."""
         if self.enabled:
-            ev = torch.cuda.Event(enable_timing=True)
+            ev = self.event()
             ev.record()
             self._pending = (ev, [(name, float(nbytes))])
 
@@ -105,7 +154,7 @@ class LaunchTimer:
 
     def end_batch(self):
         if self.enabled:
-            ev = torch.cuda.Event(enable_timing=True)
+            ev = self.event()
             ev.record()
             self.batch_marks.append(ev)
             self.batch += 1
@@ -258,6 +307,9 @@ def main():
     ap.add_argument("--unet-dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--compute", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch-events", default="fence-free", choices=["fence-free", "torch"],
+                    help="per-launch timing events: HIP events without the system-scope fence (default) or\n"
+                         "torch.cuda.Event (an L2 writeback + invalidate at every record)")
     ap.add_argument("--groups-per-call", type=int, default=1,
                     help="edit groups denoised per U-Net call (controllers.GroupBatch; a step = one such\n"
                          "batch); 1 = configs[1] as quoted")
@@ -298,7 +350,7 @@ def main():
     model = pl.SyntheticStableDiffusion(device=dev, dtype=dtype)
     prompts = pl.north_star_prompts()
     B = len(prompts)
-    timer = LaunchTimer()
+    timer = LaunchTimer(fence_free=args.launch_events == "fence-free")
     _hip.LAUNCH_OBSERVER = timer
 
     G = args.groups_per_call
@@ -367,7 +419,9 @@ def main():
                     "kernel": f"self40_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 8 waves x 2 x 32 queries, "
                               f"256-key tiles, software-pipelined 32x32 blocks)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
-                    "flop_per_launch": flops}
+                    "flop_per_launch": flops,
+                    "timing": ("HIP events around each launch on its stream, created with hipEventDisableSystemFence"
+                               if args.launch_events == "fence-free" else "torch.cuda.Event around each launch")}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.ddim_steps)
