@@ -80,23 +80,51 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
 
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   P2P_GROUP_STAMP(0)
-  // heads fastest: the 8 heads of one query tile run side by side on one XCD (xcd_remap keeps
-  // consecutive logical ids together), so the 640-byte q / o rows they share leave and enter that
-  // XCD's L2 as whole lines instead of 80-byte pieces fetched and merged per head
+  // Work order: query tiles in blocks of 4; inside a block heads fastest (the 8 heads of one query
+  // tile side by side on one XCD -- xcd_remap keeps consecutive logical ids together -- so the
+  // 640-byte q / o rows they share move as whole lines), then the block's tiles, then the groups,
+  // which alternate between the last (edit) and the first (uncond) ones: runs of 4 x H = 32
+  // workgroups change group.  With groups slowest (round 3) whole XCDs ran only edit-group
+  // workgroups (~20 % longer than plain ones, tools/group_stamps.py) and the others idled at the
+  // end; runs of 32 also pair the two workgroups resident on a CU across kinds, as far as the
+  // measurement tells: in the pipeline 22.9 -> 20.8 us at G1/G7 (runs of 8 tile-heads: 22.2;
+  // profiles/r04/group_order_r04ac/)
   int qt, h, rest;
 #ifdef P2P_EXPERIMENTS
-  if (a.variant == 126) {   // A/B: query tiles fastest (the previous order)
+  if (a.variant == 126) {   // A/B: query tiles fastest (round 2's order)
     qt = logical % a.n_qtiles;
     h = (logical / a.n_qtiles) % a.H;
     rest = logical / a.n_qtiles / a.H;
-  } else
-#endif
-  {
+  } else if (a.variant == 177) {   // A/B: heads, then query tiles, then groups (round 3's order)
     h = logical % a.H;
     qt = (logical / a.H) % a.n_qtiles;
     rest = logical / a.H / a.n_qtiles;
+  } else
+#endif
+  {
+    const int nfb = a.n_qtiles / 4;             // full blocks of 4 query tiles
+    const int per_full = 4 * a.H * a.n_groups;
+    if (logical < nfb * per_full) {
+      const int t = logical - (logical / per_full) * per_full;
+      h = t % a.H;
+      const int u = t / a.H;
+      qt = (logical / per_full) * 4 + (u & 3);
+      rest = u >> 2;
+    } else {                                    // the partial last block (n_qtiles % 4 tiles)
+      const int r = a.n_qtiles - nfb * 4;
+      const int t = logical - nfb * per_full;
+      h = t % a.H;
+      const int u = t / a.H;
+      qt = nfb * 4 + u % r;
+      rest = u / r;
+    }
   }
-  const int gi = a.n_groups - 1 - rest;   // edit groups sit last: dispatch them first
+  // rest 0, 1, 2, 3, ... -> groups G-1, 0, G-2, 1, ...: edit groups (last in the batch) and plain
+  // ones alternate
+  int gi = (rest & 1) == 0 ? a.n_groups - 1 - (rest >> 1) : (rest >> 1);
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 177) gi = a.n_groups - 1 - rest;   // (round 3: edit groups first)
+#endif
   const int first = a.grp_first[gi];
   const int count = a.grp_count[gi];
   const char* const prog = static_cast<const char*>(a.grp_prog[gi]);

@@ -20,6 +20,18 @@ from p2p_amd.tokenizer import default_tokenizer  # noqa: E402
 NWG, W, SLOTS = 2048, 4, 24
 
 
+def group_of(logical, nq, H, G):
+    """cross_group_kernel's group index of a logical workgroup id (p2p_cross.hip work order: blocks
+    of 4 query tiles; heads, then tiles, then groups alternating last / first)."""
+    nfb, per_full = nq // 4, 4 * H * G
+    if logical < nfb * per_full:
+        rest = (logical % per_full) // H // 4
+    else:
+        r = nq - nfb * 4
+        rest = ((logical - nfb * per_full) // H) // r
+    return G - 1 - rest // 2 if rest % 2 == 0 else rest // 2
+
+
 def run(name, P, d, store):
     N, H, K, B = 8, 8, 77, 4
     C = H * d
@@ -48,7 +60,7 @@ def run(name, P, d, store):
     nq = (P + 127) // 128
     nwg = min(NWG, nq * H * 2)
     s = s[:nwg]
-    gi = 1 - np.arange(nwg) // (nq * H)             # group index (cond group first; heads fastest)
+    gi = np.array([group_of(i, nq, H, 2) for i in range(nwg)])   # the kernel's work order
     print(f"== {name}: P={P} d={d} store={store}: {nwg} workgroups")
     for label, sel in (("edit group", gi == 1), ("uncond group", gi == 0)):
         ss = s[sel]
