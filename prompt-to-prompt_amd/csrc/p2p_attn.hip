@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
                "s"(a.o), "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv),
                "s"(a.bso), "s"(a.scale_log2));
   // Launches of one round of workgroups (<= 512: G2-G6, every workgroup resident at once):
-  // entries fastest, then heads -- xcd_remap keeps consecutive ids on one XCD, so the source's Q
+  // entries fastest (rotated, below), then heads -- xcd_remap keeps consecutive ids on one XCD, so the source's Q
   // rows that a tile's three edit workgroups re-read (for P0) and the tile's q / o lines stay in
   // that XCD's L2 (in the pipeline, rocprof: G2/G6 21.4 -> 20.1 us, d = 160 21.7 -> 20.9 us;
   // profiles/r04/cross_order_r04p/).  Larger launches: heads fastest, then query tiles, edits
@@ -1114,7 +1114,14 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   } else
 #endif
   if (gridDim.x <= 512) {
-    rest = logical % a.N;
+    // the second 32 of every 64 ids rotate the entries by N/2, so the two workgroups a CU holds
+    // (ids i and i + 32 of an XCD's chunk, as the group kernel's order measured) pair an edit or
+    // source entry with an uncond one instead of two edits: G2/G6 19.8 -> 18.5 us in the pipeline
+    // (profiles/r04/cross_pairing_r04ae/; experiments variant 179 = without the rotation)
+    rest = (logical % a.N + ((logical >> 5) & 1) * (a.N >> 1)) % a.N;
+#ifdef P2P_EXPERIMENTS
+    if (a.variant == 179) rest = logical % a.N;
+#endif
     h = (logical / a.N) % a.H;
     qt = logical / a.N / a.H;
   } else {
