@@ -1117,8 +1117,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     // the second 32 of every 64 ids rotate the entries by N/2, so the two workgroups a CU holds
     // (ids i and i + 32 of an XCD's chunk, as the group kernel's order measured) pair an edit or
     // source entry with an uncond one instead of two edits: G2/G6 19.8 -> 18.5 us in the pipeline
-    // (profiles/r04/cross_pairing_r04ae/; experiments variant 179 = without the rotation)
-    rest = (logical % a.N + ((logical >> 5) & 1) * (a.N >> 1)) % a.N;
+    // (profiles/r04/cross_pairing_r04ae/; experiments variant 179 = without the rotation).  The
+    // rotation is constant over each run of N ids only when N divides 32 -- otherwise (N = 64:
+    // eight groups per call) two runs would map onto the same entries -- so only then
+    const int rot = (32 % a.N == 0) ? ((logical >> 5) & 1) * (a.N >> 1) : 0;
+    rest = (logical % a.N + rot) % a.N;
 #ifdef P2P_EXPERIMENTS
     if (a.variant == 179) rest = logical % a.N;
 #endif

@@ -330,6 +330,8 @@ CROSS_GROUP_CASES = [
     (256, 160, 77, 16, 8, "group"),                                   # d = 160 (16 heads to reach the bar)
     (1024, 80, 77, 8, 1, "entry"), (256, 160, 77, 8, 2, "entry"),     # G2-G4 at configs[1]: per-entry
     (64, 160, 77, 8, 1, "entry"), (100, 80, 96, 8, 2, "entry"), (333, 40, 33, 8, 1, "entry"),
+    (64, 160, 77, 8, 8, "entry"),   # N = 64 entries in a 512-workgroup launch: the per-entry work order's
+                                    # rotation must stay a bijection when N does not divide 32
 ]
 
 

@@ -61,7 +61,8 @@ def run(name, P, d, store, blend):
     # the kernel's work order: entries fastest for launches of <= 512 workgroups, else heads
     # fastest, then query tiles (edits first either way)
     ids = np.arange(nwg)
-    ent = N - 1 - ((ids % N + ((ids >> 5) & 1) * (N // 2)) % N if nwg <= 512 else ids // (nq * H))
+    rot = ((ids >> 5) & 1) * (N // 2) if 32 % N == 0 else 0
+    ent = N - 1 - ((ids % N + rot) % N if nwg <= 512 else ids // (nq * H))
     t0 = s[:, :, 0]
     print(f"== {name}: P={P} d={d} store={store} blend={blend}: {nwg} workgroups")
     plain = ent < B + 1 if not store else ent < B
