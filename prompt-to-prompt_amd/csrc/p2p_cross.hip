@@ -502,16 +502,20 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
 // launches cross_attn_kernel instead
 // The workgroup walks the group's entries one after another, so it only pays where the grid
 // still fills the chip: >= 2 workgroups per CU (G1/G7: 2 groups x 8 heads x 32 query tiles).
-// Smaller grids (the 32x32 / 16x16 / 8x8 layers) keep the per-entry kernel's parallelism.
+// Smaller grids (the 32x32 / 16x16 / 8x8 layers) keep the per-entry kernel's parallelism, and so
+// do d = 80 / 160 at any size: with eight groups per U-Net call (configs[3], 1024 workgroups at
+// G2/G6) the group kernel -- four entries with their map stores walked in sequence -- measured
+// 228.5 us per launch against the per-entry kernel's 131.4 (profiles/r04/group_vs_entry_r04aj/);
+// at d = 40 it stays ahead (146.9 vs 215.0 us).  (The d = 80 / 160 instantiations remain in the
+// experiments build, variants 122 / 123.)
 bool cross_group_eligible(const CrossArgs& a, int d) {
   if (a.edit_terms || a.K > P2P_MAX_KEYS_CROSS) return false;
-  if (d != 40 && d != 80 && d != 160) return false;
   const int wgs = a.n_groups * a.H * ((a.P + 127) / 128);
 #ifdef P2P_EXPERIMENTS
   if (a.variant == 120) return false;   // A/B: always the per-entry kernel
-  if (a.variant == 122 || a.variant == 123) return true;   // A/B: always the group kernel (123: stamps)
+  if (a.variant == 122 || a.variant == 123) return d == 40 || d == 80 || d == 160;   // A/B: always the group kernel (123: stamps)
 #endif
-  return wgs >= 512;
+  return d == 40 && wgs >= 512;
 }
 
 int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
@@ -520,11 +524,11 @@ int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
     case 40:
       if (a.variant == 127) return (int)launch_group<40, 8>(a, st);   // A/B: 8-wave workgroups
       return (int)launch_group<40, 4>(a, st);
+    case 80: return (int)launch_group<80, 4>(a, st);
+    case 160: return (int)launch_group<160, 4>(a, st);
 #else
     case 40: return (int)launch_group<40, 4>(a, st);
 #endif
-    case 80: return (int)launch_group<80, 4>(a, st);
-    case 160: return (int)launch_group<160, 4>(a, st);
     default: return P2P_E_HEAD_DIM;
   }
 }

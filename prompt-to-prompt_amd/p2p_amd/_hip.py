@@ -237,11 +237,11 @@ def self_attn(q, k, v, o, heads, scale, compute="bf16", qk_src=None, store=None,
 def cross_group_dispatch(t: AttnTensors, groups) -> bool:
     """Whether p2p_cross_attn_fwd runs cross_group_kernel for these arguments: the rule of
     run_cross / cross_group_eligible (p2p_attn.hip, p2p_cross.hip) -- bf16 inputs and compute, no
-    term-plane program, K <= 96, d in {40, 80, 160}, and >= 512 workgroups (groups x heads x
-    128-row query tiles).  Labels only (bench.py); the library decides."""
+    term-plane program, K <= 96, d = 40, and >= 512 workgroups (groups x heads x 128-row query
+    tiles).  Labels only (bench.py); the library decides."""
     if t.io_dtype != P2P_DTYPE_BF16 or t.compute != P2P_COMPUTE_BF16 or t.n_key > MAX_KEYS_CROSS:
         return False
-    if t.head_dim not in (40, 80, 160):
+    if t.head_dim != 40:
         return False
     for grp in groups:
         prog, count = grp[2], int(grp[1])

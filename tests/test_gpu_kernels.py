@@ -323,11 +323,11 @@ def _edit_mapper(B, K, weight=0.5):
 # cross_group_eligible), so the group-kernel cases are sized to clear that bar
 CROSS_GROUP_CASES = [
     (4096, 40, 77, 8, 1, "group"), (4096, 40, 77, 8, 2, "group"),     # G1/G7
-    (1024, 80, 77, 8, 4, "group"),                                    # G2/G6 as configs[3] batches it
-    (1000, 80, 77, 8, 4, "group"),                                    # ragged P (rows past P in the store RMW)
-    (1000, 80, 96, 8, 4, "group"),                                    # K = 96: no short key tail
+    (4000, 40, 96, 8, 2, "group"),                                    # ragged P, K = 96: no short key tail
     (4000, 40, 33, 8, 1, "group"),                                    # K = 33, ragged P
-    (256, 160, 77, 16, 8, "group"),                                   # d = 160 (16 heads to reach the bar)
+    (1024, 80, 77, 8, 4, "entry"),                                    # G2/G6 as configs[3] batches it: the
+    (1000, 80, 77, 8, 4, "entry"),                                    # per-entry kernel at d = 80 / 160 at any
+    (256, 160, 77, 16, 8, "entry"),                                   # size (measured faster, p2p_cross.hip)
     (1024, 80, 77, 8, 1, "entry"), (256, 160, 77, 8, 2, "entry"),     # G2-G4 at configs[1]: per-entry
     (64, 160, 77, 8, 1, "entry"), (100, 80, 96, 8, 2, "entry"), (333, 40, 33, 8, 1, "entry"),
     (64, 160, 77, 8, 8, "entry"),   # N = 64 entries in a 512-workgroup launch: the per-entry work order's
@@ -342,7 +342,7 @@ def test_cross_group_kernel_bf16(cuda, case):
     dispatch rule): [uncond groups | cond groups], each cond group a source + 3 dense Replace
     edits against its OWN source (main.py:185-193), the cond maps kept and accumulated over two
     calls, LocalBlend word sums folded in, against fp32 einsum on the same bf16 inputs.  The group
-    kernel is covered at d = 40 / 80 / 160, ragged P, K = 96 (no short tail) and K = 33."""
+    kernel (d = 40 only) is covered at ragged P, K = 96 (no short tail) and K = 33."""
     from p2p_amd import programs
     P, d, K, H, n_groups, kernel = case
     B = 4
