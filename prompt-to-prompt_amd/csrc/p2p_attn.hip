@@ -1095,14 +1095,17 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.N), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v),
                "s"(a.o), "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv),
                "s"(a.bso), "s"(a.scale_log2));
-  // Launches of one round of workgroups (<= 512: G2-G6, every workgroup resident at once):
-  // entries fastest (rotated, below), then heads -- xcd_remap keeps consecutive ids on one XCD, so the source's Q
+  // Entries fastest (rotated, below), then heads -- xcd_remap keeps consecutive ids on one XCD, so the source's Q
   // rows that a tile's three edit workgroups re-read (for P0) and the tile's q / o lines stay in
   // that XCD's L2 (in the pipeline, rocprof: G2/G6 21.4 -> 20.1 us, d = 160 21.7 -> 20.9 us;
-  // profiles/r04/cross_order_r04p/).  Larger launches: heads fastest, then query tiles, edits
-  // dispatched first (whole q / o lines per XCD, as in cross_group_kernel)
+  // profiles/r04/cross_order_r04p/)
   int qt, h, rest;
+  // (every launch size: with eight groups per call, N = 64, entries fastest also took G2/G6 134 ->
+  // 115 us and d = 160 84 -> 72 us against heads fastest, profiles/r04/cross_order_large_r04am/;
+  // experiments variant 182 = round 3's order above 512 workgroups)
+  bool one_round = true;
 #ifdef P2P_EXPERIMENTS
+  if (a.variant == 182) one_round = gridDim.x <= 512;
   if (a.variant == 126) {   // A/B: query tiles fastest (round 2's order)
     qt = logical % a.n_qtiles;
     h = (logical / a.n_qtiles) % a.H;
@@ -1113,7 +1116,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     rest = logical / a.H / a.n_qtiles;
   } else
 #endif
-  if (gridDim.x <= 512) {
+  if (one_round) {
     // the second 32 of every 64 ids rotate the entries by N/2, so the two workgroups a CU holds
     // (ids i and i + 32 of an XCD's chunk, as the group kernel's order measured) pair an edit or
     // source entry with an uncond one instead of two edits: G2/G6 19.8 -> 18.5 us in the pipeline

@@ -58,11 +58,11 @@ def run(name, P, d, store, blend):
     nq = (P + 127) // 128
     nwg = nq * H * N
     s = s[:nwg]
-    # the kernel's work order: entries fastest for launches of <= 512 workgroups, else heads
-    # fastest, then query tiles (edits first either way)
+    # the kernel's work order: entries fastest (rotated by N/2 in the second 32 of every 64 ids
+    # when N divides 32), then heads, then query tiles
     ids = np.arange(nwg)
     rot = ((ids >> 5) & 1) * (N // 2) if 32 % N == 0 else 0
-    ent = N - 1 - ((ids % N + rot) % N if nwg <= 512 else ids // (nq * H))
+    ent = N - 1 - (ids % N + rot) % N
     t0 = s[:, :, 0]
     print(f"== {name}: P={P} d={d} store={store} blend={blend}: {nwg} workgroups")
     plain = ent < B + 1 if not store else ent < B
