@@ -41,18 +41,30 @@ class FenceFreeEvent:
     the timing-only event that avoids "the cost of cache writeback and invalidation, and the
     performance impact of those actions on the execution of following work".  The timer reads
     the events only after torch.cuda.synchronize(), so the fence is not needed for correctness.
-    Same record()/elapsed_time() surface as torch.cuda.Event; torch's own HIP runtime (already
-    loaded: libamdhip64.so.7) creates and records them."""
+    Same record()/elapsed_time() surface as torch.cuda.Event; the events are created and recorded
+    by the HIP runtime torch itself loaded (found in this process's mappings, whatever its soname)
+    and destroyed with the object."""
     _hip = None
+
+    @staticmethod
+    def _runtime_path():
+        """The libamdhip64 torch has mapped into this process (torch links it; no fixed soname)."""
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and os.path.basename(parts[5]).startswith("libamdhip64.so"):
+                    return parts[5]
+        raise RuntimeError("no HIP runtime (libamdhip64) mapped into this process")
 
     @classmethod
     def _lib(cls):
         if cls._hip is None:
             import ctypes
-            L = ctypes.CDLL("libamdhip64.so.7")
+            L = ctypes.CDLL(cls._runtime_path())
             L.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
             L.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
             L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            L.hipEventDestroy.argtypes = [ctypes.c_void_p]
             cls._hip = L
         return cls._hip
 
@@ -63,6 +75,11 @@ class FenceFreeEvent:
         rc = self._lib().hipEventCreateWithFlags(ctypes.byref(self.ev), 0x20000000)   # hipEventDisableSystemFence
         if rc != 0:
             raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
+
+    def __del__(self):
+        if self.ev.value and self._hip is not None:
+            self._hip.hipEventDestroy(self.ev)
+            self.ev = self._ctypes.c_void_p()
 
     def record(self):
         rc = self._lib().hipEventRecord(self.ev, ctypes_stream())
@@ -116,7 +133,8 @@ class LaunchTimer:
 
     def _names(self, kind, t, info):
         flop = 4.0 * t.n_query * t.n_key * t.n_heads * t.head_dim * t.n_batch
-        out = [("attn", flop), (f"attn:{kind}:P{t.n_query}:d{t.head_dim}", flop)]
+        geo = f"{kind}:P{t.n_query}:d{t.head_dim}"
+        out = [("attn", flop), (f"attn:{geo}", flop), (f"bytes:{geo}", self._bytes(kind, t, info))]
         if kind == "self" and t.n_query == self.n_query and info["stored"] == 0:
             out.append(("dominant", flop))
         if t.n_query == 1024 and info["stored"] > 0 and info["accumulate"]:
@@ -179,15 +197,38 @@ class LaunchTimer:
         tot_flop = sum(w for _, _, w, _ in recs)
         achieved = tot_flop / (tot_ms * 1e-3) / 1e12
         by = []
+        kind_ms, kind_flop, kind_bytes = {}, {}, {}
         for name in sorted(k for k in self.rec if k.startswith("attn:")):
             avg_ms, flop, n = self.summary(name)
+            _, nbytes, _ = self.summary("bytes:" + name[5:])
             tf = flop / (avg_ms * 1e-3) / 1e12
+            gbps = nbytes / (avg_ms * 1e-3) / 1e9
             d = {"geometry": name[5:], "launches": n, "avg_launch_ms": avg_ms, "flop_per_launch": flop,
-                 "achieved_tflops": tf, "frac": tf / peak, "share_of_attn_time": avg_ms * n / tot_ms}
+                 "achieved_tflops": tf, "frac": tf / peak, "share_of_attn_time": avg_ms * n / tot_ms,
+                 "algorithmic_bytes_per_launch": nbytes, "achieved_gbps": gbps, "hbm_frac": gbps / HBM_PEAK_GBPS}
             if name in self.cross_group_kernel:
                 d["kernel"] = "cross_group_kernel" if self.cross_group_kernel[name] else "cross_attn_kernel"
             by.append(d)
+            kind = name.split(":")[1]
+            kind_ms[kind] = kind_ms.get(kind, 0.0) + avg_ms * n
+            kind_flop[kind] = kind_flop.get(kind, 0.0) + flop * n
+            kind_bytes[kind] = kind_bytes.get(kind, 0.0) + nbytes * n
+        # the self kernels are MFMA work (judged by their MFMA fraction), the cross kernels (K = 77:
+        # 3.6 % of the FLOP) are q / o / map traffic (judged by their HBM fraction)
+        self_ms = kind_ms.get("self")
+        by_kind = {
+            "self": None if not self_ms else {
+                "bound": "mfma", "achieved": kind_flop["self"] / (self_ms * 1e-3) / 1e12, "peak": peak,
+                "unit": "TFLOP/s", "frac": kind_flop["self"] / (self_ms * 1e-3) / 1e12 / peak,
+                "ms_per_unet_call": self_ms / unet_calls if unet_calls else None},
+            "cross": None if not kind_ms.get("cross") else {
+                "bound": "hbm", "achieved": kind_bytes["cross"] / (kind_ms["cross"] * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": kind_bytes["cross"] / (kind_ms["cross"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                "ms_per_unet_call": kind_ms["cross"] / unet_calls if unet_calls else None},
+        }
         return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                "by_kind": by_kind,
                 "launches": len(recs), "attn_ms_total": tot_ms,
                 "attn_ms_per_unet_call": tot_ms / unet_calls if unet_calls else None,
                 "flop_per_unet_call": tot_flop / unet_calls if unet_calls else None,

@@ -18,7 +18,7 @@
 #     smallab:<v1,v2,..>     tools/small_bench.py (G2/G3/G4 self-attention), one process per variant
 #     stamps:<tool>:<v>      a clock-stamp tool (tools/<tool>.py) under P2P_SELF_VARIANT=v (experiments lib)
 #     pmcs:<tag>:<script>:<args>  tools/gpu_pmc.sh over any launcher script (comma-separated args)
-#     py:<script>[:<args>]   python -u <script> <args>
+#     py:<script>[:<a1,a2,..>]  python -u <script> <a1> <a2> ..
 set -u
 export TMPDIR=/tmp
 tag=$1; shift
@@ -80,7 +80,7 @@ for step in "$@"; do
       grep -E "p2p.*(FETCH_SIZE|WRITE_SIZE)" gpurun_out/pmc/${ptag}_summary.txt || true ;;
     py)
       script=${arg%%:*}; sargs=""; [ "$script" != "$arg" ] && sargs=${arg#*:}
-      run 1100 "$out/py_$(basename "$script" .py).log" python -u "$script" $sargs
+      run 1100 "$out/py_$(basename "$script" .py).log" python -u "$script" ${sargs//,/ }
       tail -15 "$out/py_$(basename "$script" .py).log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
