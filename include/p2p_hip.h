@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 13
+#define P2P_ABI_VERSION 14
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -32,7 +32,15 @@ extern "C" {
 #define P2P_PROGRAM_REC_BYTES (2 * 4 * P2P_PROGRAM_COLS + 8 * P2P_PROGRAM_TMAX * P2P_PROGRAM_COLS)
 #define P2P_PROGRAM_HEADER_BYTES 32
 #define P2P_PROGRAM_DENSE 96 /* dense mapper tile: f16 [DENSE][DENSE] per edit              */
-enum { P2P_PROGRAM_F_DENSE = 1 }; /* p2p_group.flags: the program carries the dense f16 tile  */
+enum {
+  P2P_PROGRAM_F_DENSE = 1, /* p2p_group.flags: the program carries the dense f16 tile           */
+  /* p2p_group.flags (ABI 14), a per-call hint: for this call's alpha row every edit's blend
+   * coefficient A[w] = alpha[w] * post[w] * c_rep[w] + 1 - alpha[w] is 0 (a Replace or Reweight
+   * step inside cross_replace_steps, main.py:189), so P_e' = R and the edit entries' own Q K^T
+   * softmax, Q and K are not needed -- the bf16 dense kernels then load only their V.  The
+   * kernel re-derives A from the program and falls back to the full edit if the hint is wrong. */
+  P2P_GROUP_F_R_ONLY = 2
+};
 
 enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };
 enum { P2P_COMPUTE_BF16 = 0, P2P_COMPUTE_F32 = 1 };

@@ -1099,42 +1099,18 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // rows that a tile's three edit workgroups re-read (for P0) and the tile's q / o lines stay in
   // that XCD's L2 (in the pipeline, rocprof: G2/G6 21.4 -> 20.1 us, d = 160 21.7 -> 20.9 us;
   // profiles/r04/cross_order_r04p/)
-  int qt, h, rest;
   // (every launch size: with eight groups per call, N = 64, entries fastest also took G2/G6 134 ->
-  // 115 us and d = 160 84 -> 72 us against heads fastest, profiles/r04/cross_order_large_r04am/;
-  // experiments variant 182 = round 3's order above 512 workgroups)
-  bool one_round = true;
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 182) one_round = gridDim.x <= 512;
-  if (a.variant == 126) {   // A/B: query tiles fastest (round 2's order)
-    qt = logical % a.n_qtiles;
-    h = (logical / a.n_qtiles) % a.H;
-    rest = logical / a.n_qtiles / a.H;
-  } else if (a.variant == 149) {   // A/B: heads fastest at every size (round 3's order)
-    h = logical % a.H;
-    qt = (logical / a.H) % a.n_qtiles;
-    rest = logical / a.H / a.n_qtiles;
-  } else
-#endif
-  if (one_round) {
-    // the second 32 of every 64 ids rotate the entries by N/2, so the two workgroups a CU holds
-    // (ids i and i + 32 of an XCD's chunk, as the group kernel's order measured) pair an edit or
-    // source entry with an uncond one instead of two edits: G2/G6 19.8 -> 18.5 us in the pipeline
-    // (profiles/r04/cross_pairing_r04ae/; experiments variant 179 = without the rotation).  The
-    // rotation is constant over each run of N ids only when N divides 32 -- otherwise (N = 64:
-    // eight groups per call) two runs would map onto the same entries -- so only then
-    const int rot = (32 % a.N == 0) ? ((logical >> 5) & 1) * (a.N >> 1) : 0;
-    rest = (logical % a.N + rot) % a.N;
-#ifdef P2P_EXPERIMENTS
-    if (a.variant == 179) rest = logical % a.N;
-#endif
-    h = (logical / a.N) % a.H;
-    qt = logical / a.N / a.H;
-  } else {
-    h = logical % a.H;
-    qt = (logical / a.H) % a.n_qtiles;
-    rest = logical / a.H / a.n_qtiles;
-  }
+  // 115 us and d = 160 84 -> 72 us against heads fastest, profiles/r04/cross_order_large_r04am/)
+  // The second 32 of every 64 ids rotate the entries by N/2, so the two workgroups a CU holds
+  // (ids i and i + 32 of an XCD's chunk, as the group kernel's order measured) pair an edit or
+  // source entry with an uncond one instead of two edits: G2/G6 19.8 -> 18.5 us in the pipeline
+  // (profiles/r04/cross_pairing_r04ae/).  The rotation is constant over each run of N ids only
+  // when N divides 32 -- otherwise (N = 64: eight groups per call) two runs would map onto the
+  // same entries -- so only then
+  const int rot = (32 % a.N == 0) ? ((logical >> 5) & 1) * (a.N >> 1) : 0;
+  const int rest = (logical % a.N + rot) % a.N;
+  const int h = (logical / a.N) % a.H;
+  const int qt = logical / a.N / a.H;
   const int n = a.N - 1 - rest;  // the edits sit last in the batch: dispatch them first
   // one dependent kernel-argument load decides the path (every a.field read is a scalar memory
   // round trip; chains of them cost ~1 us at the start of every workgroup)
@@ -1145,6 +1121,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   const int first = n - b;
   const bool edit = (info >> 16) & 1;
   const bool stored = (info >> 17) & 1;
+  // p2p_group.flags P2P_GROUP_F_R_ONLY (dense edits): this call's alpha makes every blend
+  // coefficient A = alpha post c_rep + 1 - alpha zero (a Replace / Reweight step inside
+  // cross_replace_steps, main.py:189), so P' = R B: the entry's own Q K^T softmax is not needed and
+  // neither are its Q and K -- only its V (checked again from the coefficients below)
+  const bool r_only = (info >> 18) & 1;
   const int p0w = qt * 32 * WAVES + wave * 32;
   const int p = p0w + qi;
   const bool prow = p < a.P;
@@ -1306,17 +1287,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // launch issues its prologue loads at once, and 10 MB of touches (G2/G6) in that burst delayed
   // every workgroup's first round trip (in the pipeline, rocprof: G2/G6 20.0 -> 19.1 us, d = 160
   // 20.7 -> 20.4; no touches at all: 19.8 / 20.6; profiles/r04/cross_touch_r04r/).  Experiments:
-  // variant 147 = with the prologue (before), 148 = never
   // Mode 3 goes further: after the first barrier the wave reads its rows of the running sum (and
   // its LocalBlend word-sum entries) into registers, so the store epilogue only adds and writes.
   // (bf16 inputs only: the f32-input instantiations have no registers to spare for the rows)
-  int touch_when = std::is_same<IO, uint16_t>::value ? 3 : 1;   // 0: touches with the prologue,
-                        // 1: touches after the first barrier, 2: never, 3: the values themselves
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 147) touch_when = 0;
-  if (a.variant == 148) touch_when = 2;
-  if (a.variant == 156) touch_when = 1;
-#endif
+  // 1: touches after the first barrier, 3: the values themselves
+  constexpr int touch_when = std::is_same<IO, uint16_t>::value ? 3 : 1;
   constexpr int kRmwF4 = 32 * KR / 4;
   f32x4_t rmwbuf[(kRmwF4 + 63) / 64];
   float bsum_old = 0.f;
@@ -1374,8 +1349,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     }
   };
 
-  // K (and V) of entry e: global -> registers (load_kv), registers -> LDS (store_kv)
-  auto load_kv = [&](int e, Chunk8<IO> (&kc)[NCH], Chunk8<IO> (&vc)[NCH], bool withV) {
+  // K (and V) of entry e: global -> registers (load_kv), registers -> LDS (store_kv); withK = false:
+  // V only (an R_ONLY edit)
+  auto load_kv = [&](int e, Chunk8<IO> (&kc)[NCH], Chunk8<IO> (&vc)[NCH], bool withV, bool withK = true) {
     const IO* kp = static_cast<const IO*>(a.k) + (int64_t)e * a.bsk + h * D;
     const IO* vp = static_cast<const IO*>(a.v) + (int64_t)e * a.bsv + h * D;
 #pragma unroll
@@ -1384,19 +1360,19 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
       if (cidx < K * CPR) {
-        kc[i].load(kp + (int64_t)row * a.ldk + ch * 8);
+        if (withK) kc[i].load(kp + (int64_t)row * a.ldk + ch * 8);
         if (withV) vc[i].load(vp + (int64_t)row * a.ldv + ch * 8);
       }
     }
   };
-  auto store_kv = [&](const Chunk8<IO> (&kc)[NCH], const Chunk8<IO> (&vc)[NCH], bool withV) {
+  auto store_kv = [&](const Chunk8<IO> (&kc)[NCH], const Chunk8<IO> (&vc)[NCH], bool withV, bool withK = true) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
       if (cidx < K * CPR) {
-        MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
+        if (withK) MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
         if (withV) vc[i].store(Vs + row * VS + ch * 8);
       }
     }
@@ -1467,8 +1443,8 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   f32x16_t Rd[KB];
   int dense_flags = 3;   // dense edits: the blend halves in use (set from the coefficients)
   // dense edits: this entry's own K / V are loaded together with the source's prologue loads, so
-  // the workgroup waits one memory round trip instead of two (variant 138 of an experiments
-  // build: own K / V staged after the R phase, as before)
+  // the workgroup waits one memory round trip instead of two (measured against staging them
+  // after the R phase: profiles/r03/cross_store/cross_bench_own_kv_*.log)
   Chunk8<IO> kc1[kDenseOk ? NCH : 1], vc1[kDenseOk ? NCH : 1];
   typename MQ::frag qf1[kDenseOk ? NKT : 1];   // (and its own Q rows)
   bool own_early = false;
@@ -1501,13 +1477,12 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     Chunk8<IO> kc0[NCH], vc0[NCH];
     load_kv(first, kc0, vc0, false);
     load_q(first, qf);
-    own_early = true;
-#ifdef P2P_EXPERIMENTS
-    if (a.variant == 138) own_early = false;
-#endif
+    own_early = !r_only;
     if (own_early) {
       load_kv(n, kc1, vc1, true);
       load_q(n, qf1);
+    } else if (r_only) {
+      load_kv(n, kc1, vc1, true, false);   // own V only
     }
     finish_prologue();
     P2P_CROSS_STAMP(19)
@@ -1528,6 +1503,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     }
     P2P_CROSS_STAMP(21)
     store_kv(kc0, vc0, false);
+    // R_ONLY: the own V goes to its LDS image now (the P0 / R phase reads only K and the mapper),
+    // so no second staging phase follows
+    if (r_only) store_kv(kc1, vc1, true, false);
     P2P_CROSS_STAMP(22)
     __syncthreads();
     if (touch_when == 1 || touch_when == 3) touch();
@@ -1574,7 +1552,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     if (own_early) {
 #pragma unroll
       for (int t = 0; t < NKT; ++t) qf[t] = qf1[t];
-    } else {
+    } else if (!r_only || (dense_flags & 1)) {
       load_q(n, qf);
     }
     __syncthreads();  // every wave is done with the source K tile and the mapper tile
@@ -1611,13 +1589,25 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     if (!edit) finish_prologue();   // (the edit paths called it with their first loads)
     store_kv(kc, vc, true);
   };
+  bool own_staged = true;
   if constexpr (kDenseOk) {
-    if (own_early) store_kv(kc1, vc1, true);
-    else stage_own();
+    if (own_early) {
+      store_kv(kc1, vc1, true);
+    } else if (r_only) {
+      // own V is in LDS already; own K only if the coefficients contradict the host's flag
+      own_staged = (dense_flags & 1) != 0;
+      if (own_staged) {
+        Chunk8<IO> kc[NCH], vc[NCH];
+        load_kv(n, kc, vc, false);
+        store_kv(kc, vc, false);
+      }
+    } else {
+      stage_own();
+    }
   } else {
     stage_own();
   }
-  __syncthreads();
+  if (own_staged) __syncthreads();   // (workgroup-uniform: every wave reads the same coefficients)
   if (!edit && (touch_when == 1 || touch_when == 3)) touch();
   P2P_CROSS_STAMP(11)
   if (!dense || (dense_flags & 1)) {
@@ -1786,12 +1776,7 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
   if (a.n_maps > 0)  // the lse feeds stored maps: exact f32 row sums
     hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
   else if constexpr (kOnes && MP::kElemBytes == 2) {
-    // O only (no lse): no per-tile max (P2P_SELF_VARIANT 16 in an experiments build keeps it)
-#ifdef P2P_EXPERIMENTS
-    if (a.lse == nullptr && a.variant == 16)
-      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
-    else
-#endif
+    // O only (no lse): no per-tile max
     if (a.lse == nullptr)
       hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false, true>), grid, block, 0, st, b);
     else
@@ -1816,80 +1801,40 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
     // d = 40 on the bf16 pipe, nothing but O wanted (G1/G7 without kept maps or autograd)
     if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && a.P > 64) {
       constexpr bool kF16 = MQ::planes == 1 && sizeof(IO) == 2;
-      // bf16 inputs: the software-pipelined F16-form kernel (p2p_self40.hip); experiments
-      // variants 40-45 select the round-2 multi-block kernel instead
+      // bf16 inputs: the software-pipelined F16-form kernel (p2p_self40.hip)
       if constexpr (kF16)
-        if (self40_eligible(a, 40) && (a.variant == 0 || a.variant >= 60)) return (hipError_t)run_self40(a, 40, st);
-      if (a.variant == 0 && a.P >= 2048) {
+        if (self40_eligible(a, 40)) return (hipError_t)run_self40(a, 40, st);
+      if (a.P >= 2048) {
         // f32 inputs (split-bf16 Q K^T, two K planes): the multi-block kernel, 128-key tiles;
         // bf16 inputs with K < 256: the same with the F16 form
         if constexpr (MQ::planes == 1) launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st);
         else launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st);
         return hipGetLastError();
       }
-#ifdef P2P_EXPERIMENTS
-      // A/B timing of the round-2 shapes: 40 = the bf16 form (v_fma per score), 44 = F16 form,
-      // 128-key tiles, 17 = 64-key tiles x 4 waves, 27 = 256-key tiles, 28 = 4-wave workgroups,
-      // 41 = 64-key tiles x 8 waves, 42/43 = sub-block-pipelined Q K^T (128/256-key tiles),
-      // 45 = 43 with static priority for waves 4-7
-      switch (a.variant) {
-        case 40: launch_multi<IO, MQ, D, 128, 8, 2>(a, st); return hipGetLastError();
-        case 44: launch_multi<IO, MQ, D, 128, 8, 2, kF16>(a, st); return hipGetLastError();
-        case 17: launch_multi<IO, MQ, D, 64, 4, 2, kF16>(a, st); return hipGetLastError();
-        case 27:
-          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16>(a, st); return hipGetLastError(); }
-          break;
-        case 28: launch_multi<IO, MQ, D, 128, 4, 2, kF16>(a, st); return hipGetLastError();
-        case 41: launch_multi<IO, MQ, D, 64, 8, 2, kF16>(a, st); return hipGetLastError();
-        case 42: launch_multi<IO, MQ, D, 128, 8, 2, kF16, true>(a, st); return hipGetLastError();
-        case 43:
-          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true>(a, st); return hipGetLastError(); }
-          break;
-        case 45:
-          if constexpr (MQ::planes == 1) { launch_multi<IO, MQ, D, 256, 8, 2, kF16, true, true>(a, st); return hipGetLastError(); }
-          break;
-        default: break;
-      }
-#endif
     }
   }
   if constexpr (MP::kElemBytes == 2 && D == 80 && MQ::planes == 1 && sizeof(IO) == 2) {
     // d = 80, bf16 inputs, nothing but O wanted (G2/G6 without kept maps or autograd): the
     // software-pipelined kernel of p2p_self40.hip in its bf16 form
-    if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && self40_eligible(a, 80) &&
-        (a.variant == 0 || a.variant >= 91))
+    if (mode == MODE_FUSED && a.lse == nullptr && a.n_maps == 0 && self40_eligible(a, 80))
       return (hipError_t)run_self40(a, 80, st);
   }
   if constexpr (MP::kElemBytes == 2 && D == 160 && MQ::planes == 1 && sizeof(IO) == 2) {
     // d = 160, bf16 inputs, O only (the 16x16 / 8x8 layers without kept maps or autograd): the
-    // waves of a 32-query workgroup split the keys (p2p_selfsplit.hip); variant 121 (experiments
-    // build) keeps the per-tile kernel below for A/B timing
-    if (mode == MODE_FUSED && self_split_eligible(a, D) && a.variant != 121) return (hipError_t)run_self_split(a, D, st);
-    if (mode == MODE_FUSED && self_ring_eligible(a, D) && a.variant != 134) return (hipError_t)run_self_ring(a, D, st);
+    // waves of a 32-query workgroup split the keys (p2p_selfsplit.hip, K <= 128), or the per-tile
+    // kernel with its 4-stage DMA ring (K = 256)
+    if (mode == MODE_FUSED && self_split_eligible(a, D)) return (hipError_t)run_self_split(a, D, st);
+    if (mode == MODE_FUSED && self_ring_eligible(a, D)) return (hipError_t)run_self_ring(a, D, st);
   }
   if (mode == MODE_FUSED) {
-    // tile shape of the hot kernel (P2P_SELF_VARIANT selects alternatives for A/B timing)
     if constexpr (BK == 64 && (D == 40 || D == 80)) {
       if (a.P > 64) {
-        // default: 8 waves x 32 query rows per workgroup, 64-key tiles (measured best at
-        // d = 40 and within 2 % of best at d = 80: tools/attn_bench.py, profiles/)
-#ifdef P2P_EXPERIMENTS
-        switch (a.variant) {
-          case 1: launch_fused<IO, MQ, MP, D, 64, 4>(a, st); return hipGetLastError();
-          case 2: launch_fused<IO, MQ, MP, D, 128, 4>(a, st); return hipGetLastError();
-          case 3: launch_fused<IO, MQ, MP, D, 128, 8>(a, st); return hipGetLastError();
-          default: break;
-        }
-#endif
+        // 8 waves x 32 query rows per workgroup, 64-key tiles (measured best at d = 40 and within
+        // 2 % of best at d = 80: tools/attn_bench.py, profiles/)
         launch_fused<IO, MQ, MP, D, 64, 8>(a, st);
         return hipGetLastError();
       }
     }
-#ifdef P2P_EXPERIMENTS
-    // 124: 64-key tiles at d >= 128 (half the per-tile round trips; 84 KB of LDS)
-    if constexpr (D >= 128 && MP::kElemBytes == 2)
-      if (a.variant == 124 && a.P > 64) { launch_fused<IO, MQ, MP, D, 64, 4>(a, st); return hipGetLastError(); }
-#endif
     if (a.P <= 64) launch_fused<IO, MQ, MP, D, BK, 2>(a, st);
     else launch_fused<IO, MQ, MP, D, BK, 4>(a, st);
     return hipGetLastError();
@@ -1928,11 +1873,6 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
 
 template <typename IO, typename MQ, typename MP, int D>
 static hipError_t launch_cross_d(const CrossArgs& a, hipStream_t st) {
-#ifdef P2P_EXPERIMENTS
-  // 50: two-wave workgroups (twice the workgroups) for the small bf16 grids (d <= 80)
-  if constexpr (MP::kElemBytes == 2 && D <= 80)
-    if (a.variant == 50) return launch_cross_w<IO, MQ, MP, D, 2>(a, st);
-#endif
   return launch_cross_w<IO, MQ, MP, D, (MP::kElemBytes == 4 && D >= 128) ? 2 : 4>(a, st);
 }
 
@@ -1958,14 +1898,7 @@ static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(n_kgroups * b.n_qtiles * a.H * a.n_maps), block(256);
   // non-temporal running-sum accesses (the map streams through once per step: -7.5 % at G2 with
-  // the maps HBM-resident; two key blocks per step measured +2 %, not instantiated).
-  // P2P_SELF_VARIANT=6 (experiments build) keeps plain accesses for A/B timing.
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 6) {
-    hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, false>), grid, block, 0, st, b, kw, n_kgroups);
-    return hipGetLastError();
-  }
-#endif
+  // the maps HBM-resident; two key blocks per step measured +2 %, not instantiated)
   hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
   return hipGetLastError();
 }
@@ -1976,14 +1909,7 @@ static hipError_t launch_self_probs_d(const SelfArgs& a, hipStream_t st) {
   const int kw = ((a.K + 3) / 4 + 31) / 32 * 32;  // keys per wave: a quarter of the row
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(b.n_qtiles * a.H * a.N), block(256);
-  // non-temporal probability stores (a write-once stream: G1 1.33 -> 1.04 ms, G2 118 -> 104 us);
-  // P2P_SELF_VARIANT=7 (experiments build) keeps plain stores for A/B timing
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 7) {
-    hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, false>), grid, block, 0, st, b, kw);
-    return hipGetLastError();
-  }
-#endif
+  // non-temporal probability stores (a write-once stream: G1 1.33 -> 1.04 ms, G2 118 -> 104 us)
   hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, true>), grid, block, 0, st, b, kw);
   return hipGetLastError();
 }

@@ -172,7 +172,9 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
     const int g = a.ent_group[n];
     const int b = n - a.grp_first[g];
     const bool edit = a.grp_prog[g] != nullptr && b > 0;
-    a.ent_info[n] = g | (b << 8) | (edit ? 1 << 16 : 0) | (a.store_slot[n] >= 0 ? 1 << 17 : 0);
+    const bool r_only = edit && (a.grp_flags[g] & P2P_PROGRAM_F_DENSE) && (a.grp_flags[g] & P2P_GROUP_F_R_ONLY);
+    a.ent_info[n] = g | (b << 8) | (edit ? 1 << 16 : 0) | (a.store_slot[n] >= 0 ? 1 << 17 : 0) |
+                    (r_only ? 1 << 18 : 0);
   }
   a.store = any_store ? store : nullptr;
   a.store_accumulate = store_accumulate ? 1 : 0;

@@ -90,17 +90,6 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   // measurement tells: in the pipeline 22.9 -> 20.8 us at G1/G7 (runs of 8 tile-heads: 22.2;
   // profiles/r04/group_order_r04ac/)
   int qt, h, rest;
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 126) {   // A/B: query tiles fastest (round 2's order)
-    qt = logical % a.n_qtiles;
-    h = (logical / a.n_qtiles) % a.H;
-    rest = logical / a.n_qtiles / a.H;
-  } else if (a.variant == 177) {   // A/B: heads, then query tiles, then groups (round 3's order)
-    h = logical % a.H;
-    qt = (logical / a.H) % a.n_qtiles;
-    rest = logical / a.H / a.n_qtiles;
-  } else
-#endif
   {
     const int nfb = a.n_qtiles / 4;             // full blocks of 4 query tiles
     const int per_full = 4 * a.H * a.n_groups;
@@ -121,10 +110,7 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   }
   // rest 0, 1, 2, 3, ... -> groups G-1, 0, G-2, 1, ...: edit groups (last in the batch) and plain
   // ones alternate
-  int gi = (rest & 1) == 0 ? a.n_groups - 1 - (rest >> 1) : (rest >> 1);
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 177) gi = a.n_groups - 1 - rest;   // (round 3: edit groups first)
-#endif
+  const int gi = (rest & 1) == 0 ? a.n_groups - 1 - (rest >> 1) : (rest >> 1);
   const int first = a.grp_first[gi];
   const int count = a.grp_count[gi];
   const char* const prog = static_cast<const char*>(a.grp_prog[gi]);
@@ -521,9 +507,7 @@ bool cross_group_eligible(const CrossArgs& a, int d) {
 int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
 #ifdef P2P_EXPERIMENTS
-    case 40:
-      if (a.variant == 127) return (int)launch_group<40, 8>(a, st);   // A/B: 8-wave workgroups
-      return (int)launch_group<40, 4>(a, st);
+    case 40: return (int)launch_group<40, 4>(a, st);
     case 80: return (int)launch_group<80, 4>(a, st);
     case 160: return (int)launch_group<160, 4>(a, st);
 #else

@@ -52,7 +52,8 @@ struct CrossArgs {
   int store_slot[P2P_MAX_BATCH];
   int ent_group[P2P_MAX_BATCH];  // prompt group of every batch entry
   // per entry, packed so ONE kernel-argument load after n decides the path: group (bits 0-7),
-  // position in the group (8-15), edits (16), keeps its maps (17)
+  // position in the group (8-15), edits (16), keeps its maps (17), dense edit whose group is
+  // flagged P2P_GROUP_F_R_ONLY (18)
   int ent_info[P2P_MAX_BATCH];
   int grp_first[P2P_MAX_GROUPS];
   int grp_count[P2P_MAX_GROUPS];

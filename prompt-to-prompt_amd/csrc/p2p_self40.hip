@@ -87,9 +87,15 @@ __device__ unsigned long long g_s40_stamps[kStampWgs * 8 * kStampSlots];
 
 // One workgroup = WAVES waves x QB query blocks of 32 rows = 32*QB*WAVES queries of one (entry,
 // head); BK-key tiles, double-buffered in LDS.
+//
+// FORM bits (measured-and-dropped variants live in git history, DESIGN.md §4 cites their logs):
+//   1        LEAN fragment buffering (one K and one V fragment set per wave)
+//   16       clock stamps (experiments build only)
+//   128      split staging: waves 0..WAVES/2-1 stage K (the f16 conversion), the rest V
+//   256/512/16384  the younger half holds priority 1 for 3 of every 4 steps
+//   8388608  K's f16 range check as a packed-u16 maximum
 template <int kD, int WAVES, int QB, int BK, bool SCHED, int FORM>
-// (FORM bit 4096: a 4-wave workgroup sized for two per CU -- two waves per SIMD, <= 256 VGPRs)
-__global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 : 1) void self40_kernel(SelfArgs a) {
+__global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(SelfArgs a) {
   using G = Geom<kD>;
   constexpr bool kF16 = G::F16;
   constexpr int kNKT = G::NKT;
@@ -109,47 +115,19 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int NCH = (BK * kCPR + NT - 1) / NT;
   constexpr int KBUF = BK * kKS;
   constexpr int VBUF = BK * kVS;
-  // FORM bit 524288 (key split): wave w and w + WAVES/2 hold the same queries and take the two
-  // halves of every tile's keys, combined through LDS at the end -- twice the waves per SIMD for
-  // grids of one workgroup per CU without halving the reuse of each K / V fragment
-  constexpr bool kKSplit = (FORM & 524288) != 0;
-  constexpr int WQ = kKSplit ? WAVES / 2 : WAVES;   // query waves
-  constexpr int NSBW = kKSplit ? NSB / 2 : NSB;     // 32-key sub-blocks per wave and tile
-  static_assert(!kKSplit || (NSB % 2 == 0 && WAVES % 2 == 0), "key split");
-  constexpr int X = NSBW * QB;   // pipeline steps (32x32 blocks) per tile
+  constexpr int X = NSB * QB;   // pipeline steps (32x32 blocks) per tile
   constexpr float kThr = 8.0f;  // exact path: defer-max threshold (log2 units)
   // FORM bit 128 (split staging): waves 0..WAVES/2-1 stage K (the f16 conversion), the younger
   // half -- the VALU-arbitration loser -- stages V (copy only); else every wave stages both
   constexpr bool kSplit = (FORM & 128) != 0;
   constexpr int SCH = (BK * kCPR + NT / 2 - 1) / (NT / 2);   // chunks per thread, split staging
   constexpr int CMAX = kSplit ? SCH : NCH;
-  // staging writes: chunk i of the next tile at step kHalf + i (X - kHalf) / n (several per step
+  // staging writes: chunk i of the next tile at step kWs + i (X - kWs) / n (several per step
   // when there are more chunks than steps), from the middle of the tile on -- the loads issued at
   // its start have landed by then
-  constexpr int kHalf = X / 2;
-  // FORM bit 131072: the per-tile barrier split into LDS counters (tsync).  tsync[b] counts the
-  // waves that have written their chunks of a tile into buffer b, tsync[2 + b] the waves done
-  // reading a tile from it; a wave waits only for the chunks it reads next or for the readers of
-  // the buffer it overwrites, so the waves of a workgroup drift up to (X - kWe) steps apart.  The
-  // staging window moves to [X/4, X/2) (bit 262144: [X/2, 3X/4)) to leave that slack
-  constexpr bool kFlagSync = (FORM & 131072) != 0;
-  constexpr int kWs = !kFlagSync ? kHalf : (FORM & 262144) ? X / 2 : X / 4;
-  constexpr int kWe = !kFlagSync ? X : (FORM & 262144) ? (3 * X) / 4 : X / 2;
-  static_assert(kWe > kWs, "staging window");
+  constexpr int kWs = X / 2;
+  constexpr int kWe = X;
   auto nchunks = [](auto role) { return decltype(role)::value == 0 ? NCH : SCH; };
-  // FORM bit 1048576 (DMA staging, bf16 form only): K / V tiles go global -> LDS by
-  // global_load_lds (no staging VGPRs, no staging VALU, no LDS write instructions): the next tile's
-  // DMA is issued at the top of a tile into the other buffer and waited (vmcnt(0)) before the tile
-  // barrier.  The DMA writes whole 16-byte slots of every LDS row, padding included, so V's row-sum
-  // column D cannot live in the tile: the P V operand's columns D.. come from a constant [4][16]
-  // block (column 0 = 1, the rest 0) instead.  With the key split (bit 524288) this is the d = 80
-  // kernel with two waves per SIMD that register staging could not fit in 256 VGPRs.
-  constexpr bool kDma = (FORM & 1048576) != 0;
-  static_assert(!kDma || (!kF16 && kDK == kD && (kDV - kD) <= 16), "DMA staging: bf16 form, no K padding read");
-  constexpr int KSL = kKS / 8, VSL = kVS / 8;   // 16-byte slots per K / V row in LDS
-  constexpr int kDmaK = BK * KSL / 64, kDmaV = BK * VSL / 64;   // DMA instructions per tile
-  static_assert(!kDma || ((BK * KSL) % 64 == 0 && (BK * VSL) % 64 == 0), "whole DMA instructions per tile");
-  __shared__ __attribute__((aligned(16))) uint16_t vones[kDma ? 64 : 8];
   // K and V tile buffers; after the last tile the same LDS holds each wave's output rows (epilogue)
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * KBUF + 2 * VBUF];
   uint16_t* const Ks = smem;
@@ -157,7 +135,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   constexpr int kOS = kD + 8;   // output row in LDS: 16-byte aligned, rows on distinct banks
   static_assert(WAVES * 32 * QB * kOS <= 2 * KBUF + 2 * VBUF, "epilogue rows fit the tile buffers");
   __shared__ int wg_flag;
-  __shared__ int tsync[4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -177,23 +154,14 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 #endif
   };
   stamp(0);
-  // FORM bit 8192: heads fastest -- one XCD then runs all heads of a query tile (whole q / o lines
-  // in its L2) and, with xcd_remap's contiguous chunks, all tiles of one entry (its K / V once)
-  int qt, h, n;
-  if constexpr ((FORM & 8192) != 0) {
-    h = logical % a.H;
-    qt = (logical / a.H) % a.n_qtiles;
-    n = logical / a.H / a.n_qtiles;
-  } else {
-    qt = logical % a.n_qtiles;
-    h = (logical / a.n_qtiles) % a.H;
-    n = logical / a.n_qtiles / a.H;
-  }
+  // query tiles fastest: with xcd_remap's contiguous chunks one XCD runs all tiles of an (entry,
+  // head), so that head's K / V come from its L2 (heads fastest measured no faster and raised the
+  // reads, profiles/r03 variant 128)
+  const int qt = logical % a.n_qtiles;
+  const int h = (logical / a.n_qtiles) % a.H;
+  const int n = logical / a.n_qtiles / a.H;
   const int src = a.qk_src[n];
-  const int khalf = kKSplit ? __builtin_amdgcn_readfirstlane(wave) / WQ : 0;   // key half (key split)
-  const int wq = kKSplit ? wave - khalf * WQ : wave;
-  const int sbo = khalf * NSBW;                   // first sub-block of this wave in a tile
-  const int pw = (qt * WQ + wq) * 32 * QB;        // first query of this wave
+  const int pw = (qt * WAVES + wave) * 32 * QB;   // first query of this wave
   const int K = a.K;
   const float c = a.scale_log2;
 
@@ -213,11 +181,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       *reinterpret_cast<short8_t*>(Vs + r * kVS + kD + 8 * j) =
           short8_t{(short)(j == 0 ? 0x3F80 : 0), 0, 0, 0, 0, 0, 0, 0};
   }
-  if constexpr (kDma)
-    if (tid < 64) vones[tid] = (tid & 15) == 0 ? (uint16_t)0x3F80 : (uint16_t)0;   // [4][16]: column 0 = 1
   if (tid == 0) wg_flag = 0;
-  if constexpr (kFlagSync)
-    if (tid < 4) tsync[tid] = 0;
 
   // ---- Q fragments: lane (qi, hh) of block b, k step t holds Q[p][16t + 8hh .. +7]
   bool ovf = false;
@@ -263,8 +227,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // K and V of the chunk; split staging: role 1 = K chunks of threads 0..NT/2-1, role 2 = V
   // chunks of the others, each thread holding SCH of them in kreg)
   const bool young = __builtin_amdgcn_readfirstlane(wave) >= WAVES / 2;
-  // FORM bit 65536: the roles of the two halves swapped (the younger half converts K)
-  const bool vrole = ((FORM & 65536) != 0) ? !young : young;
+  const bool vrole = young;
   const int stid = kSplit ? tid - (young ? NT / 2 : 0) : tid;   // (position within the half)
   const int sstride = kSplit ? NT / 2 : NT;
   short8_t kreg[CMAX], vreg[NCH];
@@ -352,34 +315,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     else go(std::integral_constant<int, 1>{});
   };
 
-  // DMA of tile kt into buffer buf: instruction i (of kDmaK K + kDmaV V) moves 64 16-byte slots;
-  // wave w issues i = w, w + WAVES, ...  Padding slots fetch a valid chunk of the same row, rows
-  // past K the last key (finite data; their scores are masked, their P is 0)
-  const uint32_t smem_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  auto dma_tile = [&](int kt, int buf) __attribute__((always_inline)) {
-    if constexpr (kDma) {
-      const int w0 = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-      for (int j = 0; j < (kDmaK + kDmaV + WAVES - 1) / WAVES; ++j) {
-        const int i = w0 + j * WAVES;
-        if (i < kDmaK) {
-          const int slot = i * 64 + lane;
-          const int row = slot / KSL;
-          const int ch = min(slot - row * KSL, kCPR - 1);
-          const int key = min(kt * BK + row, K - 1);
-          glds16(kp + (int64_t)key * a.ldk + ch * 8,
-                 __builtin_amdgcn_readfirstlane(smem_lds + (uint32_t)(buf * KBUF * 2 + i * 1024)));
-        } else if (i < kDmaK + kDmaV) {
-          const int slot = (i - kDmaK) * 64 + lane;
-          const int row = slot / VSL;
-          const int ch = min(slot - row * VSL, kCPR - 1);
-          const int key = min(kt * BK + row, K - 1);
-          glds16(vp + (int64_t)key * a.ldv + ch * 8,
-                 __builtin_amdgcn_readfirstlane(smem_lds + (uint32_t)((2 * KBUF + buf * VBUF) * 2 + (i - kDmaK) * 1024)));
-        }
-      }
-    }
-  };
   const int ntiles = (K + BK - 1) / BK;
   const int nfull = K / BK;
   f32x16_t O[QB][kNDT];
@@ -398,29 +333,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int dt = 0; dt < kNDT; ++dt) {
-        if (kDma && dt == kNDT - 1) {
-          // (vt_frag's addressing; lanes whose columns are >= D read the constant block instead)
-          const int r = sb * 32 + 16 * s2 + 4 * hh + ((lane & 15) >> 2);
-          const int cc = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          typedef __attribute__((address_space(3))) short4_t lds_s4;
-          const uint16_t* plo = cc >= kD ? vones + ((lane & 15) >> 2) * 16 + (cc - kD) : Vb + r * kVS + cc;
-          const uint16_t* phi = cc >= kD ? plo : Vb + (r + 8) * kVS + cc;
-          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)plo);
-          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)phi);
-          vf[s2][dt] = short8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        } else {
-          vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
-        }
-      }
+      for (int dt = 0; dt < kNDT; ++dt) vf[s2][dt] = vt_frag<kVS>(Vb, sb * 32, s2, dt * 32, lane).v;
   };
 
-  if constexpr (kDma) {
-    dma_tile(0, 0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): Q and this wave's DMA of tile 0
-  } else {
-    stage_all(0, 0, kF16);
-  }
+  stage_all(0, 0, kF16);
   __syncthreads();
 
   // ---- reference point: the row maximum of c s over the first 32 keys (F16: Q column D is still 0)
@@ -448,41 +364,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   }
 
   stamp(1);
-  // static priority for the second-dispatched half of the waves (FORM bit 8; the condition must
-  // be provably wave-uniform, or every wave gets priority 1)
-  if constexpr ((FORM & 8) != 0)
-    if (__builtin_amdgcn_readfirstlane(wave) >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
-  // FORM bits 32/64: the waves sharing a SIMD (w, w + WAVES/2) run the same program; the older
-  // one wins VALU arbitration and reaches the tile barrier first.  The younger half takes
-  // priority 1 for the first kFlip steps of every tile, so both arrive together
-  constexpr int kFlipSel = (FORM >> 5) & 3;
-  constexpr int kFlip = kFlipSel == 1 ? X / 2 : kFlipSel == 2 ? X / 4 : kFlipSel == 3 ? (3 * X) / 4 : 0;
   bool bad = false;
-  // tsync[idx] >= target, read by one wave-uniform LDS load per poll; a poll bound that runs out
-  // (it cannot in a correct schedule: the writer of a buffer never waits on its readers' next
-  // tile) marks the wave bad, which sends the workgroup to the barrier-synchronised exact
-  // recompute instead of hanging
-  auto tsync_wait = [&](int idx, int target) __attribute__((always_inline)) {
-    asm volatile("" ::: "memory");
-    int seen = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(&tsync[idx]));
-    if (__builtin_expect(seen < target, 0)) {
-      for (int spin = 0; seen < target; ++spin) {
-        if (spin >= (1 << 16)) {
-          bad = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        seen = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(&tsync[idx]));
-      }
-    }
-    asm volatile("" ::: "memory");
-  };
-  // this wave's LDS writes (or reads) of a buffer complete, then one count
-  auto tsync_signal = [&](int idx) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) atomicAdd(&tsync[idx], 1);
-    asm volatile("" ::: "memory");
-  };
   // ---- one tile of the fast form, software-pipelined over its X blocks.  more: the next tile
   // is staged during this one (compile-time, so the tile body is one basic block); masked: keys
   // past K in this tile
@@ -491,20 +373,13 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     constexpr bool kMasked = decltype(masked)::value;
     constexpr int kNcw = nchunks(role);
     const int buf = kt & 1;
-    if constexpr (kMore) {
-      if constexpr (kDma) dma_tile(kt + 1, buf ^ 1);   // buf ^ 1 was last read before the previous barrier
-      else stage_load(kt + 1, role);
-    }
-    if constexpr (kFlagSync)
-      if (kt >= 1) tsync_wait(buf, WAVES * ((kt + 1) >> 1));   // every wave's chunks of this tile
-    const uint16_t* const Kb = Ks + buf * KBUF + sbo * 32 * kKS;   // (this wave's key half)
-    const uint16_t* const Vb = Vs + buf * VBUF + sbo * 32 * kVS;
+    if constexpr (kMore) stage_load(kt + 1, role);
+    const uint16_t* const Kb = Ks + buf * KBUF;
+    const uint16_t* const Vb = Vs + buf * VBUF;
     // LEAN: one K and one V fragment set, each re-read right after its last reader (K of
     // sub-block sb+1 after the last Q K^T on sb, V of sb after the last P V on sb-1)
     constexpr bool kLean = (FORM & 1) != 0;
-    constexpr bool kLeanK = kLean && (FORM & 4) == 0;   // FORM bit 4: LEAN V, double-buffered K
-    constexpr bool kValuFirst = (FORM & 2) != 0;
-    constexpr bool kSplitTrans = (FORM & 4194304) != 0;
+    constexpr bool kLeanK = kLean;
     short8_t kf[2][kNKT];
     short8_t vf[2][2][kNDT];
     f32x16_t S[2];
@@ -534,35 +409,26 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       float e[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        // (FORM bits 67108864 / 134217728: timing probes of the experiments build -- no scale-and-
-        // shift fma / no exponential; the results are wrong)
-        float s = (kF16 || (FORM & 67108864) != 0) ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
+        float s = kF16 ? S[x & 1][r] : fmaf(S[x & 1][r], c, -m_ref[b]);
         if constexpr (kMasked)
-          if (kt * BK + (sbo + sb) * 32 + acc_row(r, hh) >= K) s = -INFINITY;
-        e[r] = (FORM & 134217728) != 0 ? s : fast_exp2(s);
+          if (kt * BK + sb * 32 + acc_row(r, hh) >= K) s = -INFINITY;
+        e[r] = fast_exp2(s);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) pf[x & 1][s2][j] = (short)f2bf(e[8 * s2 + j]);
     };
-    if constexpr (kFlip > 0)
-      if (young) __builtin_amdgcn_s_setprio(1);
     qk(0);
     if constexpr (SCHED) __builtin_amdgcn_sched_barrier(0);
     static_for<X>([&](auto xc) __attribute__((always_inline)) {
       constexpr int x = decltype(xc)::value;
-      if constexpr (kFlagSync && kMore && x == kWs)   // every wave done with tile kt - 1 (same buffer)
-        if (kt >= 1) tsync_wait(2 + (buf ^ 1), WAVES * ((kt + 1) >> 1));
-      if constexpr (kFlagSync && kMore && x == kWe) tsync_signal(buf ^ 1);
-      if constexpr (kFlip > 0 && x == kFlip)
-        if (young) __builtin_amdgcn_s_setprio(0);
       // FORM bit 256: the younger half holds priority 1 for the first half of every kAlt steps
       // (bit 512: kAlt = 4, else 2), so the two waves of a SIMD share the VALU evenly
-      // (bits 16384 / 32768, with 512: priority 1 for 3 of every 4 steps / 1 of every 4)
+      // (bit 16384, with 512: priority 1 for 3 of every 4 steps)
       if constexpr ((FORM & 256) != 0) {
         constexpr int kAlt = (FORM & 512) ? 4 : 2;
-        constexpr int kOn = (FORM & 16384) ? 3 : (FORM & 32768) ? 1 : kAlt / 2;
+        constexpr int kOn = (FORM & 16384) ? 3 : kAlt / 2;
         if constexpr (x % kAlt == 0) { if (young) __builtin_amdgcn_s_setprio(1); }
         if constexpr (x % kAlt == kOn) { if (young) __builtin_amdgcn_s_setprio(0); }
       }
@@ -570,10 +436,10 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       // K of sub-block sb+1: LEAN after this step's Q K^T when it was the last one on sb
       // (b == QB-2: Q K^T of block x+1 = (sb, QB-1)), else early into the other slot
       // (QB == 1: block x+1 is already on sb+1, so its K is read at the start of this step)
-      constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSBW;
+      constexpr bool kRdK = (kLeanK ? b == (QB >= 2 ? QB - 2 : 0) : b == 0) && sb + 1 < NSB;
       constexpr bool kRdKEarly = kLeanK && kRdK && QB == 1;
       // V: LEAN reads V(sb) after this step's P V on block x-1 = (sb-1, QB-1); else V(sb+1) early
-      constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSBW);
+      constexpr bool kRdV = kLean ? (b == 0 && sb >= 1) : (b == (QB > 1 ? 1 : 0) && sb + 1 < NSB);
       // the next tile's chunks go to the other buffer over the second half of the tile (every
       // wave has passed the barrier that ended the tile which last read that buffer)
       // chunks [c0, c1) of this thread are written in this step
@@ -581,7 +447,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       constexpr bool kInW = x >= kWs && x < kWe;
       constexpr int c0 = kInW ? ((x - kWs) * kNcw + kWn - 1) / kWn : 0;
       constexpr int c1 = kInW ? ((x + 1 - kWs) * kNcw + kWn - 1) / kWn : 0;
-      constexpr bool kStw = kMore && c1 > c0 && !kDma;
+      constexpr bool kStw = kMore && c1 > c0;
       constexpr bool kStwK = kStw && decltype(role)::value != 2;   // the write converts K
       if constexpr (!kLeanK && kRdK) read_k(Kb, sb + 1, kf[(sb + 1) & 1]);
       if constexpr (kRdKEarly) read_k(Kb, sb + 1, kf[0]);
@@ -610,19 +476,8 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
           constexpr int te = (ne * (i + 1)) / nm - (ne * i) / nm;
           constexpr int tv = (nv * (i + 1)) / nm - (nv * i) / nm;
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if constexpr (kValuFirst) {
-            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
-            __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
-          } else if constexpr (kSplitTrans) {
-            // FORM bit 4194304: the slot's VALU between its exponentials, so a pack rarely sits
-            // right behind the exp it reads (the trans -> VALU hazard's s_nop)
-            __builtin_amdgcn_sched_group_barrier(0x400, (te + 1) / 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
-            __builtin_amdgcn_sched_group_barrier(0x400, te - (te + 1) / 2, 0);
-          } else {
-            __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
-          }
+          __builtin_amdgcn_sched_group_barrier(0x400, te, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, tv, 0);
           if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, (nr * (i + 1)) / nm - (nr * i) / nm, 0);
           if constexpr (kLeanK && kRdK && !kRdKEarly && i >= nq && i < nq + kNKT)
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -653,7 +508,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     for (int b = 0; b < QB; ++b) {
       const float lsum = lsums[b];
       bad |= !(lsum < INFINITY);
-      constexpr float kResc = (FORM & 2048) ? 0x1p100f : 0x1p64f;   // FORM bit 2048: probe threshold
+      constexpr float kResc = 0x1p64f;
       if (__builtin_expect(__any(lsum > kResc), 0)) {
         if (lsum > kResc) {
           const float mnew = kF16 ? (float)(_Float16)(m_ref[b] + 64.f) : m_ref[b] + 64.f;
@@ -668,9 +523,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
         }
       }
     }
-    if constexpr (kDma && kMore) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's DMA of tile kt + 1
-    if constexpr (kFlagSync) tsync_signal(2 + buf);   // this wave's reads of buf are done
-    else __syncthreads();
+    __syncthreads();
     stamp(3 + 2 * kt);
   };
   constexpr std::false_type kNo{};
@@ -696,7 +549,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
         for (int r = 0; r < 16; ++r) nf = __builtin_fmaf(O[b][dt][r], 0.f, nf);   // NaN iff some O is inf/NaN
     bad |= !(nf == 0.f);
     if constexpr (kU16Max) ovf |= kmag.x >= 0x4780 || kmag.y >= 0x4780;
-    const bool any_bad = __any(bad || ovf) || (FORM & 1024) != 0;   // FORM bit 1024: always recompute
+    const bool any_bad = __any(bad || ovf);
     if (lane == 0 && any_bad) atomicOr(&wg_flag, 1);
   }
   __syncthreads();
@@ -714,7 +567,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
     for (int kt = 0; kt < ntiles; ++kt) {
       stage_all(kt, 0, false);
       __syncthreads();
-      for (int sb = sbo; sb < sbo + NSBW; ++sb) {
+      for (int sb = 0; sb < NSB; ++sb) {
         short8_t kf[kNKT];
         short8_t vf[2][kNDT];
         read_k(Ks, sb, kf);
@@ -752,37 +605,6 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
       }
       __syncthreads();
     }
-#pragma unroll
-    for (int b = 0; b < QB; ++b) m_ref[b] = m_run[b];   // (the key-split combine's reference)
-  }
-
-  if constexpr (kKSplit) {
-    // ---- key split: the second half's O (row sums included) and reference points through LDS
-    // (the tile buffers are dead), one query block per round; the first half rescales both to
-    // the larger reference and adds
-    float* const xo = reinterpret_cast<float*>(smem) + wq * (kNDT * 16 * 64 + 64);
-    static_assert(WQ * (kNDT * 16 * 64 + 64) * 4 <= (2 * KBUF + 2 * VBUF) * 2, "combine slots fit the tile buffers");
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      if (khalf == 1) {
-#pragma unroll
-        for (int dt = 0; dt < kNDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) xo[(dt * 16 + r) * 64 + lane] = O[b][dt][r];
-        xo[kNDT * 16 * 64 + lane] = m_ref[b];
-      }
-      __syncthreads();
-      if (khalf == 0) {
-        const float m1 = xo[kNDT * 16 * 64 + lane];
-        const float mx = fmaxf(m_ref[b], m1);
-        const float f0 = fast_exp2(m_ref[b] - mx), f1 = fast_exp2(m1 - mx);
-#pragma unroll
-        for (int dt = 0; dt < kNDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) O[b][dt][r] = O[b][dt][r] * f0 + xo[(dt * 16 + r) * 64 + lane] * f1;
-      }
-      __syncthreads();
-    }
   }
 
   stamp(36);
@@ -790,8 +612,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
   // (64 cache lines) per instruction; the wave writes its rows to LDS instead (the tile buffers
   // are dead: every wave has passed the last tile's barrier) and stores them back as contiguous
   // 16-byte chunks, consecutive lanes along a row
-  if (kKSplit && khalf != 0) return;   // (key split: the first half holds the combined rows)
-  uint16_t* const orow = smem + wq * (32 * QB * kOS);
+  uint16_t* const orow = smem + wave * (32 * QB * kOS);
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const float l = __shfl(O[b][kLdt][kLr], lane & 31);
@@ -828,8 +649,7 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES >= 8 || (FORM & 4096) != 0) ? 2 
 template <int D, int WAVES, int QB, int BK, bool SCHED = true, int FORM = 0>
 hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
-  constexpr int WQ = (FORM & 524288) != 0 ? WAVES / 2 : WAVES;   // query waves (key split: half)
-  b.n_qtiles = (a.P + 32 * QB * WQ - 1) / (32 * QB * WQ);
+  b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
   hipLaunchKernelGGL((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
@@ -844,6 +664,7 @@ bool self40_eligible(const SelfArgs& a, int d) {
 }
 
 // variant: 0 = production shapes; the experiments build also honours the A/B shapes below
+// (every other measured shape is in git history; DESIGN.md §4 and profiles/ hold the logs)
 int run_self40(const SelfArgs& a, int d, hipStream_t st) {
 #ifdef S40_ONLY
   return (int)launch<S40_ONLY>(a, st);
@@ -851,34 +672,8 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
   if (d == 80) {
     switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
-      case 91: return (int)launch<80, 8, 2, 128, true, 1>(a, st);
-      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);
-      case 93: return (int)launch<80, 4, 2, 128, true, 1 | 1024>(a, st);   // exact recompute only
-      case 94: return (int)launch<80, 4, 2, 128, true, 1 | 2048>(a, st);
-      case 95: return (int)launch<80, 4, 2, 128, false, 1>(a, st);
-      case 96: return (int)launch<80, 4, 2, 128, true, 0>(a, st);
-      case 97: return (int)launch<80, 4, 1, 128, true, 1 | 4096>(a, st);
-      case 98: return (int)launch<80, 4, 1, 64, true, 1 | 4096>(a, st);
-      case 99: return (int)launch<80, 4, 2, 64, true, 1>(a, st);
-      case 100: return (int)launch<80, 2, 2, 64, true, 1 | 4096>(a, st);
-      case 101: return (int)launch<80, 8, 1, 64, true, 1>(a, st);
-      case 102: return (int)launch<80, 8, 1, 128, true, 1>(a, st);
-      case 103: return (int)launch<80, 4, 2, 128, true, 1 | 16>(a, st);   // 92 with clock stamps
+      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);        // round 3's pinned schedule
       case 164: return (int)launch<80, 4, 2, 128, false, 1 | 16>(a, st);  // default with clock stamps
-      // timing probes (wrong results): no scale-and-shift fma, no exponential, neither
-      // (profiles/r04/d80_probes_r04m.log: 29.2 / 29.2 / 28.6 / 27.2 us -- not VALU-bound)
-      case 170: return (int)launch<80, 4, 2, 128, false, 1 | 67108864>(a, st);
-      case 171: return (int)launch<80, 4, 2, 128, false, 1 | 134217728>(a, st);
-      case 172: return (int)launch<80, 4, 2, 128, false, 1 | 67108864 | 134217728>(a, st);
-      case 128: return (int)launch<80, 4, 2, 128, true, 1 | 8192>(a, st);  // default, heads fastest
-      // key split: 8 waves, wave w and w + 4 on the two key halves of each tile (two waves per SIMD)
-      case 143: return (int)launch<80, 8, 2, 128, true, 1 | 524288>(a, st);
-      case 144: return (int)launch<80, 8, 2, 128, true, 1 | 128 | 524288>(a, st);   // + split staging
-      case 145: return (int)launch<80, 8, 1, 128, true, 1 | 524288>(a, st);
-      // DMA staging (no staging VGPRs): alone, and with the key split over two waves per SIMD
-      case 150: return (int)launch<80, 4, 2, 128, true, 1 | 1048576>(a, st);
-      case 151: return (int)launch<80, 8, 2, 128, true, 1 | 524288 | 1048576>(a, st);
-      case 152: return (int)launch<80, 8, 2, 128, true, 1 | 8 | 524288 | 1048576>(a, st);
 #endif
       // d = 80 (one wave per SIMD): the compiler's own schedule (no sched_group_barrier pinning)
       // measured 0.0269 vs 0.0277-0.0278 ms at G2 (profiles/r04/ab_d80_r04f.log; variant 92 is the
@@ -888,53 +683,8 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
   }
   switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
-    case 62: return (int)launch<40, 4, 2, 128>(a, st);
-    case 64: return (int)launch<40, 4, 2, 256, false>(a, st);
-    case 61: return (int)launch<40, 4, 2, 256>(a, st);
-    case 66: return (int)launch<40, 8, 2, 256, true, 1>(a, st);   // round-3 first LEAN default
-    case 67: return (int)launch<40, 8, 2, 256, true, 3>(a, st);
-    case 68: return (int)launch<40, 4, 2, 256, true, 2>(a, st);
-    case 69: return (int)launch<40, 4, 2, 256, true, 1>(a, st);
-    case 70: return (int)launch<40, 8, 2, 128, true, 1>(a, st);
-    case 71: return (int)launch<40, 8, 2, 256, true, 1 | 16>(a, st);   // 66 with clock stamps
-    case 72: return (int)launch<40, 8, 2, 256, true, 1 | 8>(a, st);
-    case 73: return (int)launch<40, 8, 2, 256, true, 1 | 4>(a, st);
-    case 74: return (int)launch<40, 8, 2, 256, true, 1 | 32>(a, st);        // priority flip at X/2
-    case 75: return (int)launch<40, 8, 2, 256, true, 1 | 64>(a, st);        // at X/4
-    case 76: return (int)launch<40, 8, 2, 256, true, 1 | 96>(a, st);        // at 3X/4
-    case 77: return (int)launch<40, 8, 2, 256, true, 1 | 32 | 16>(a, st);   // 74 with clock stamps
-    case 78: return (int)launch<40, 8, 2, 256, true, 1 | 128>(a, st);       // split staging
-    case 79: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 32>(a, st);  // split staging + flip at X/2
-    case 80: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 16>(a, st);  // 78 with clock stamps
-    case 82: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512>(a, st);  // alternate every 4 steps
-    case 83: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 16>(a, st);   // default with clock stamps
-    // two 4-wave workgroups per CU (128-key tiles, 78 KB of LDS each): the SIMD's second wave
-    // belongs to another workgroup, so one workgroup's barrier wait overlaps the other's compute
-    case 104: return (int)launch<40, 4, 2, 128, true, 1 | 4096>(a, st);
-    case 105: return (int)launch<40, 4, 2, 128, true, 1 | 128 | 4096>(a, st);
-    case 106: return (int)launch<40, 4, 2, 64, true, 1 | 4096>(a, st);
-    case 107: return (int)launch<40, 4, 2, 128, true, 1 | 16 | 4096>(a, st);   // 104 with clock stamps
-    case 128: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 8192>(a, st);   // default, heads fastest
-    case 129: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // young prio 3/4 of steps
-    case 130: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 32768>(a, st);   // young prio 1/4
-    case 131: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 65536>(a, st);         // young half converts K
-    case 132: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 65536>(a, st);               // swap, no priority
-    // the tile barrier split into LDS counters (staging window [X/4, X/2) / [X/2, 3X/4)); 141 = 139 with stamps
-    case 139: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072>(a, st);
-    case 140: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 262144>(a, st);
-    case 141: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384 | 131072 | 16>(a, st);
-    case 142: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 131072>(a, st);   // no priority duty
-    // round 4: the exponentials split around the slot's VALU (160), the packed-u16 K range check
-    // (161), both (162)
-    case 160: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304>(a, st);
-    case 161: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608>(a, st);
-    case 162: return (int)launch<40, 8, 2, 256, true, 17281 | 4194304 | 8388608>(a, st);
     case 163: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 16>(a, st);   // default with clock stamps
-    // (165/166, round 4: two chained items per workgroup -- the next item's first tile and Q rows
-    // loaded in the item's last tile -- measured 1.5-2.6 % slower, profiles/r04/chain/; code in
-    // commit 5a2e317)
 #endif
-    case 133: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256>(a, st);   // round-3 first default
     case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // three of every four steps (round 3: 0.1867 ms vs 0.1880-0.1885 for priority on alternate step

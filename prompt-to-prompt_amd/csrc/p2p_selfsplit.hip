@@ -341,18 +341,13 @@ hipError_t launch_ring(const SelfArgs& a, hipStream_t st) {
 
 }  // namespace
 
-// d = 160, bf16 inputs, O only, K > 128: the 4-stage DMA ring (variant 134 of an experiments
-// build: the per-tile kernel of p2p_attn.hip instead)
+// d = 160, bf16 inputs, O only, K > 128: the 4-stage DMA ring
 bool self_ring_eligible(const SelfArgs& a, int d) {
   return d == 160 && a.K > 128 && a.lse == nullptr && a.n_maps == 0;
 }
 
 int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
   (void)d;
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 135) return (int)launch_ring<2>(a, st);
-  if (a.variant == 136) return (int)launch_ring<1>(a, st);
-#endif
   return (int)launch_ring<4>(a, st);
 }
 

@@ -32,7 +32,8 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 13
+ABI_VERSION = 14
+GROUP_F_R_ONLY = 2      # p2p_group.flags: every edit's blend coefficient A is 0 this call (P' = R)
 
 
 class HipError(RuntimeError):
@@ -252,18 +253,20 @@ def cross_group_dispatch(t: AttnTensors, groups) -> bool:
 
 def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, store_slot=None,
                accumulate=False):
-    """groups: list of (first, count, program_tensor|None, alpha_tensor|None[, blend]) with blend =
-    None or (sums [count, 2, lh, n_query] f32, alpha [count, n_key] f32, sub [count, n_key] | None,
-    col, lh): LocalBlend's word sums folded into the store epilogue (p2p_group.blend_*)."""
+    """groups: list of (first, count, program_tensor|None, alpha_tensor|None[, blend[, hints]]) with
+    blend = None or (sums [count, 2, lh, n_query] f32, alpha [count, n_key] f32, sub [count, n_key] |
+    None, col, lh): LocalBlend's word sums folded into the store epilogue (p2p_group.blend_*); hints:
+    per-call p2p_group.flags bits OR'ed onto the program's (GROUP_F_R_ONLY)."""
     t = make_tensors(q, k, v, o, heads, scale, compute)
     G = (Group * len(groups))()
     for i, grp in enumerate(groups):
         first, count, prog, alpha = grp[:4]
         blend = grp[4] if len(grp) > 4 else None
+        hints = int(grp[5]) if len(grp) > 5 else 0
         G[i].first, G[i].count = int(first), int(count)
         G[i].program = prog.data_ptr() if prog is not None else None
         G[i].alpha = alpha.data_ptr() if alpha is not None else None
-        G[i].flags = int(getattr(prog, "p2p_flags", 0)) if prog is not None else 0
+        G[i].flags = (int(getattr(prog, "p2p_flags", 0)) | hints) if prog is not None else 0
         G[i].n_edits = int(getattr(prog, "p2p_n_edits", 0)) if prog is not None else 0
         if blend is not None:
             sums, balpha, bsub, col, lh = blend

@@ -108,6 +108,20 @@ def as_mask(m):
     return m.materialize() if isinstance(m, FoldedBlendMask) else m
 
 
+def group_mask_tensor(masks, B, size):
+    """Per-group step masks (None = the group does not blend) as the mask-reading latent step's
+    (mask [G*B, H, W] uint8, group size, groups that blend [G] uint8) triple."""
+    masks = [as_mask(mk) for mk in masks]
+    dev = next(mk for mk in masks if mk is not None).device
+    out = torch.zeros(len(masks) * B, *size, dtype=torch.uint8, device=dev)
+    blend = torch.zeros(len(masks), dtype=torch.uint8)
+    for g, mk in enumerate(masks):
+        if mk is not None:
+            out[g * B:(g + 1) * B] = mk
+            blend[g] = 1
+    return out, B, blend.to(dev)
+
+
 def fused_blend_mask(attention_store, alpha_flat, sub_flat, th_pool, th_sub, size, folded=None):
     """LocalBlend's final mask [B, H, W] (uint8) only; the latent blend itself then runs inside
     p2p_latent_step together with the CFG combine and the DDIM step.  ``folded``: the running word
@@ -491,6 +505,9 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         self.num_self_replace = int(num_steps * self_replace_steps[0]), int(num_steps * self_replace_steps[1])
         self.local_blend = local_blend
         self._program_cache = {}
+        self._program_host = None
+        self._alpha_host = None
+        self._step_cache = {}
         self._blend_sums, self._blend_valid, self._blend_step = None, False, set()
 
     # ------------------------------------------------------------------ fused edits
@@ -501,10 +518,42 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         key = str(device)
         if key not in self._program_cache:
             try:
-                self._program_cache[key] = self._edit_program().to_device(device)
+                host = self._edit_program()
+                self._program_cache[key] = host.to_device(device)
+                self._program_host = host
             except ValueError as err:      # beyond the program tables: materialised protocol
                 raise NotFusable from err
         return self._program_cache[key]
+
+    def _cross_step(self, device, K):
+        """The cross-attention edit of this step as (program or None, p2p_group hint flags), from
+        the host copy of cross_replace_alpha[cur_step] (main.py:189) and the program's c_rep / post:
+        with B = alpha post and A = alpha post c_rep + 1 - alpha on every word of every edit,
+          * B = 0 and A = 1 everywhere (past cross_replace_steps): P' = R * 0 + P_e = P_e exactly,
+            the group runs unedited (no program: the kernels load no mapper, no source rows);
+          * A = 0 everywhere (a Replace / Reweight step inside the window): P' = R B, the edits'
+            own softmax, Q and K are dead -- GROUP_F_R_ONLY.
+        Decided once per step (the alpha table is copied to the host once)."""
+        prog = self._device_program(device)
+        alpha = self.cross_replace_alpha
+        held = self._alpha_host   # (the tensor itself, its version, host copy): identity, not id()
+        if held is None or held[0] is not alpha or held[1] != alpha._version:
+            held = self._alpha_host = (alpha, alpha._version, alpha.detach().to("cpu", torch.float64).numpy())
+            self._step_cache = {}
+        key = (self.cur_step, K)
+        hit = self._step_cache.get(key)
+        if hit is not None:
+            return (None if hit[0] else prog), hit[1]
+        host = self._program_host
+        a = held[2][self.cur_step].reshape(host.n_edits, -1)[:, :K]
+        post = host.post[:, :K].astype(np.float64)
+        crep = host.c_rep[:, :K].astype(np.float64)
+        B = a * post
+        A = B * crep + (1.0 - a)
+        plain = bool(np.all(B == 0.0) and np.all(A == 1.0))
+        hints = _hip.GROUP_F_R_ONLY if np.all(A == 0.0) else 0
+        self._step_cache[key] = (plain, hints)
+        return (None if plain else prog), hints
 
     def _fused_forward(self, q, k, v, heads, scale, is_cross, place_in_unet):
         N, P, K = q.shape[0], q.shape[1], k.shape[1]
@@ -516,13 +565,13 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
             alpha = self.cross_replace_alpha[self.cur_step]
             if K > _hip.MAX_KEYS_CROSS or alpha.shape[-1] != K or alpha.device != q.device:
                 raise NotFusable
-            prog = self._device_program(q.device)
+            prog, hints = self._cross_step(q.device, K)
         store, acc = self._store_target(is_cross, place_in_unet, n_cond, heads, P, K, q.device)
         slots = self._slots(N, n0, heads, store)
         out = torch.empty_like(q)
         if is_cross:
             blend = self._blend_fold(self._last_store_key, P, K, heads, q.device) if store is not None else None
-            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous(), blend)]
+            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous(), blend, hints)]
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
                             store_slot=slots, accumulate=acc)
         else:
@@ -709,15 +758,7 @@ class GroupBatch(AttentionControl):
                 # every blending group folded, one threshold set: the masks are built inside
                 # p2p_latent_step (one launch per step for the whole batch)
                 return masks, B
-            masks = [as_mask(mk) for mk in masks]
-            dev = next(mk for mk in masks if mk is not None).device
-            out = torch.zeros(len(masks) * B, *size, dtype=torch.uint8, device=dev)
-            blend = torch.zeros(len(masks), dtype=torch.uint8)
-            for g, mk in enumerate(masks):
-                if mk is not None:
-                    out[g * B:(g + 1) * B] = mk
-                    blend[g] = 1
-            return out, B, blend.to(dev)
+            return group_mask_tensor(masks, B, size)
 
         return True, mask_fn
 
@@ -756,7 +797,8 @@ class GroupBatch(AttentionControl):
                     if alpha.shape[-1] != K or alpha.device != q.device:
                         raise ValueError("edit tables do not match this attention call")
                     blend = m._blend_fold(store_key, P, K, heads, q.device) if store is not None else None
-                    groups.append((first, B, m._device_program(q.device), alpha.contiguous(), blend))
+                    prog, hints = m._cross_step(q.device, K)
+                    groups.append((first, B, prog, alpha.contiguous(), blend, hints))
                 else:
                     groups.append((first, B, None, None))
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,

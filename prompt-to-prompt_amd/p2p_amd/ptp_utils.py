@@ -51,10 +51,18 @@ def _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidanc
         return None
     if eps is None or not eps.is_contiguous():
         eps = torch.cat([eps_u, eps_c]).contiguous()
-    from .controllers import FoldedBlendMask
+    from .controllers import FoldedBlendMask, group_mask_tensor
     x = latents.contiguous()
+    out = torch.empty_like(x)
     mask = mask_fn(tuple(x.shape[2:])) if mask_fn is not None else None
     group_size, group_blend, blend = 0, None, None
+    folded = mask if isinstance(mask, FoldedBlendMask) else (
+        next((m for m in mask[0] if m is not None), None) if isinstance(mask, tuple) and len(mask) == 2 else None)
+    if folded is not None and not _blend_launch_ok(x, out, eps, folded):
+        # shapes the one-launch LocalBlend does not take: the mask is built by p2p_localblend and
+        # the latent step reads it (the same mask, two launches)
+        mask = folded.materialize() if isinstance(mask, FoldedBlendMask) else group_mask_tensor(
+            mask[0], mask[1], tuple(x.shape[2:]))
     if isinstance(mask, FoldedBlendMask):  # LocalBlend built inside the latent-step launch
         mask, blend = None, [mask.latent_entry()]
     elif isinstance(mask, tuple) and len(mask) == 2:   # prompt-group batch, every blending group folded
@@ -62,9 +70,18 @@ def _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidanc
         mask, group_size = None, mask[1]
     elif isinstance(mask, tuple):          # prompt-group batch: (mask, group size, groups that blend)
         mask, group_size, group_blend = mask
-    out = torch.empty_like(x)
     return _hip.latent_step(eps, x, out, model.scheduler.prev_coeffs(t), guidance_scale, mask,
                             group_size, group_blend, blend)
+
+
+def _blend_launch_ok(x, out, eps, folded) -> bool:
+    """The one-launch LocalBlend's preconditions (p2p_blend.hip run_latent_step, include/p2p_hip.h):
+    whole 4-pixel vectors (H*W % 4 == 0), 16-byte aligned x / out / eps, and a latent at least as
+    large as the map resolution (the 3x3-pooled map is nearest-upsampled onto it)."""
+    H, W = x.shape[2], x.shape[3]
+    res = int(round(folded.sums.shape[-1] ** 0.5))
+    return ((H * W) % 4 == 0 and res <= H and res <= W and res * res <= 256
+            and (x.data_ptr() | out.data_ptr() | eps.data_ptr()) % 16 == 0)
 
 
 def latent2image(vae, latents):

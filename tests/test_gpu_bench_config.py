@@ -14,7 +14,8 @@
 import pytest
 import torch
 
-from oracle_runs import cosine, oracle_controller, oracle_group, replace_group
+from oracle_runs import (EFFECT_BAR, EFFECT_BAR_BF16_UNET, base_group, check_effect, check_negative, cosine,
+                         oracle_controller, oracle_group, sharpen_attention, shifted_replace_mapper)
 from p2p_amd import config, controllers
 from p2p_amd import pipeline as pl
 
@@ -45,9 +46,11 @@ def _record_oracle_masks(olb, sink):
     return Rec()
 
 
-def test_bench_default_config_50_steps(cuda, tok):
+def _bench_config_vs_oracle(cuda, tok, gain, effect_bar):
     prompts = pl.north_star_prompts()
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    if gain != 1.0:
+        sharpen_attention(model, gain)
     x_T = pl.seed_latent(0)
     pmasks = []
     with config.compute_mode("bf16"):
@@ -63,31 +66,65 @@ def test_bench_default_config_50_steps(cuda, tok):
     print("product run done", flush=True)
     want = oracle_group(model, prompts, x_T, octrl, 50)
     cos = cosine(got, want)
-    print("bench config (bf16 U-Net + bf16 kernels) final-latent cosine per prompt:", [round(c, 6) for c in cos.tolist()])
+    print(f"bench config (bf16 U-Net + bf16 kernels, attention gain {gain}) final-latent cosine per prompt:",
+          [round(c, 6) for c in cos.tolist()])
     assert torch.isfinite(got).all()
     assert cos.min().item() >= 0.999, cos
     assert len(pmasks) == len(omasks) == 50
-    agree, n = [], 0
+    agree, cover, n = [], [], 0
     for pm, om in zip(pmasks, omasks):
         assert (pm is None) == (om is None)
         if pm is None:
             continue
         n += 1
         agree.append(((pm != 0) == om.reshape(pm.shape)).float().mean().item())
-    print(f"LocalBlend masks over {n} blended steps: min agreement {min(agree):.6f}, mean {sum(agree) / n:.6f}")
+        cover.append(om[1:].float().mean().item())
+    print(f"LocalBlend masks over {n} blended steps: min agreement {min(agree):.6f}, mean {sum(agree) / n:.6f}; "
+          f"edit-prompt mask coverage {min(cover):.3f}..{max(cover):.3f}")
     assert n == 40
-    assert sum(agree) / n >= 0.999 and min(agree) >= 0.995, agree
+    assert min(agree) >= 0.999, agree          # north star: >= 99.9 % of the pixels, at EVERY step
+    # the edit's effect, and negative controls that must fail the same bar
+    base = base_group(model, prompts, x_T, 50)
+    check_effect(f"configs[1] as benched, gain {gain}", got, want, base, effect_bar)
+    with config.compute_mode("bf16"):
+        neg_none = pl.run_edit_group(model, prompts, controllers.EmptyControl(), x_T, num_steps=50)
+        bad = pl.make_replace_controller(prompts, 50, device=cuda)
+        bad.mapper = shifted_replace_mapper(bad.mapper)
+        neg_map = pl.run_edit_group(model, prompts, bad, x_T, num_steps=50)
+        nocross = pl.make_replace_controller(prompts, 50, cross_replace_steps=0.0, device=cuda)
+        neg_cross = pl.run_edit_group(model, prompts, nocross, x_T, num_steps=50)
+    check_negative("no edit", neg_none, want, base, effect_bar)
+    check_negative("wrong mapper", neg_map, want, base, effect_bar)
+    check_negative("cross replace off", neg_cross, want, base, effect_bar)
+
+
+def test_bench_default_config_50_steps(cuda, tok):
+    """configs[1] exactly as benched (random-init weights).  The edit moves the latents by ~2 % of
+    their norm here and the two bf16 trajectories differ by ~0.8 %, so the edit-effect bar is 0.80
+    (measured 0.84-0.95; every negative control <= 0.63: profiles/r05/effect_probe.log)."""
+    _bench_config_vs_oracle(cuda, tok, 1.0, EFFECT_BAR_BF16_UNET)
+
+
+def test_bench_config_sharpened_50_steps(cuda, tok):
+    """The same pipeline with every attention logit x4 (sharpen_attention): peaky maps, as a
+    trained model's, so the edit moves the latents by ~14 % and the full 0.99 edit-effect bar
+    applies at bf16 (measured 0.994-0.998; negative controls <= 0.52)."""
+    _bench_config_vs_oracle(cuda, tok, 4.0, EFFECT_BAR)
 
 
 STEPS2 = 10
 
 
-def _config2_vs_oracle(cuda, tok, unet_dtype, steps, check_groups, per_step_bar):
+def _config2_vs_oracle(cuda, tok, unet_dtype, steps, check_groups, per_step_bar, effect_bar=EFFECT_BAR, gain=1.0,
+                       maps=True):
     """A GroupBatch of 8 Refine+Reweight groups (one U-Net call of batch 64 per step) for `steps`
-    DDIM steps; the groups in check_groups each against their own single-group oracle run."""
+    DDIM steps; the groups in check_groups each against their own single-group oracle run, with
+    the edit-effect check (effect_bar; None = not asserted) and negative controls on the first."""
     prompts = [pl.REFINE_SOURCE] + pl.REFINE_EDITS
     seeds = list(range(20, 28))
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=unet_dtype)
+    if gain != 1.0:
+        sharpen_attention(model, gain)
     with config.compute_mode("bf16"):
         members = [pl.make_refine_reweight_controller(prompts, steps, device=cuda, tokenizer=tok) for _ in seeds]
         batch = controllers.GroupBatch(members)
@@ -97,14 +134,33 @@ def _config2_vs_oracle(cuda, tok, unet_dtype, steps, check_groups, per_step_bar)
     print(f"product GroupBatch of {len(seeds)} groups x {steps} steps done", flush=True)
     B = len(prompts)
     worst_cos, worst_map = 1.0, 0.0
+    bar = effect_bar
     for g in check_groups:
         octrl = oracle_controller("refine_reweight", prompts, tok, steps, cuda)
-        want = oracle_group(model, prompts, pl.seed_latent(seeds[g]), octrl, steps)
+        x_T = pl.seed_latent(seeds[g])
+        want = oracle_group(model, prompts, x_T, octrl, steps)
         cos = cosine(got[g * B:(g + 1) * B], want)
         worst_cos = min(worst_cos, cos.min().item())
+        base = base_group(model, prompts, x_T, steps) if bar is not None else None
+        if bar is not None:
+            check_effect(f"  group {g}", got[g * B:(g + 1) * B], want, base, bar)
+        if bar is not None and g == check_groups[0]:
+            # negative controls on this group: no edit, the equalizer off, a wrong refine gather
+            with config.compute_mode("bf16"):
+                neg = {"no edit": controllers.EmptyControl(),
+                       "no reweight": pl.make_refine_reweight_controller(prompts, steps, value=1.0, device=cuda,
+                                                                         tokenizer=tok),
+                       "wrong refine mapper": pl.make_refine_reweight_controller(prompts, steps, device=cuda,
+                                                                                 tokenizer=tok)}
+                m = neg["wrong refine mapper"].prev_controller.mapper
+                shifted = m.clone()
+                shifted[:, 1:] = m[:, :-1]
+                neg["wrong refine mapper"].prev_controller.mapper = shifted
+                for name, c in neg.items():
+                    check_negative(name, pl.run_edit_group(model, prompts, c, x_T, num_steps=steps), want, base, bar)
         m = members[g]
         assert m.cur_step == octrl.cur_step == steps
-        for key in ("down_cross", "mid_cross", "up_cross"):
+        for key in ("down_cross", "mid_cross", "up_cross") if maps else ():
             ours, ref = m.attention_store[key], octrl.attention_store[key]
             assert len(ours) == len(ref), key
             for x, y in zip(ours, ref):
@@ -115,7 +171,7 @@ def _config2_vs_oracle(cuda, tok, unet_dtype, steps, check_groups, per_step_bar)
           f"cosine {worst_cos:.6f}, worst stored cross-map |diff| {worst_map:.3e} "
           f"({worst_map / steps:.2e} per accumulated step)")
     assert worst_cos >= 0.999
-    assert worst_map < per_step_bar * steps
+    assert not maps or worst_map < per_step_bar * steps
 
 
 def test_config2_f32unet_50_steps_vs_oracle(cuda, tok):
@@ -134,7 +190,18 @@ def test_config2_eight_refine_reweight_groups_vs_oracle(cuda, tok, unet_dtype):
     trajectories (measured 2.1e-3 per step; the kernel error on identical inputs is pinned per call
     in test_gpu_controllers.py::test_edits_bf16_sd_geometry[*bf16in]) -- 3e-3 there, 2e-3 with the
     f32 U-Net."""
-    _config2_vs_oracle(cuda, tok, unet_dtype, STEPS2, range(8), 2e-3 if unet_dtype == torch.float32 else 3e-3)
+    _config2_vs_oracle(cuda, tok, unet_dtype, STEPS2, range(8), 2e-3 if unet_dtype == torch.float32 else 3e-3,
+                       effect_bar=EFFECT_BAR if unet_dtype == torch.float32 else None)
+
+
+def test_config2_bf16unet_sharpened_50_steps_effect(cuda, tok):
+    """configs[2] as benched (bf16 U-Net, 8 Refine+Reweight groups in one GroupBatch, 50 steps) on
+    the sharpened weights (every logit x4, sharpen_attention), where the edits move the latents
+    by ~7-8 % and the full 0.99 edit-effect bar applies at bf16 (measured 0.994; negative controls
+    <= 0.60, profiles/r05/effect_probe.log).  Groups 0 and 7 against single-group oracle runs;
+    the stored maps are pinned by the teacher-forced test below, not compared across the two
+    bf16 trajectories here."""
+    _config2_vs_oracle(cuda, tok, torch.bfloat16, 50, (0, 7), None, effect_bar=EFFECT_BAR, gain=4.0, maps=False)
 
 
 def test_config2_bf16unet_50_steps_teacher_forced(cuda, tok):

@@ -409,3 +409,48 @@ def test_self_attention_key_split_d160(cuda, case):
     assert torch.isfinite(o.float()).all()
     bound = o_tol(v, "bf16") + 2.0 ** -8 * want.abs().max().item()
     assert (o.float() - want).abs().max().item() < bound
+
+
+@pytest.mark.parametrize("geom", [(1024, 80, 1), (256, 160, 1), (64, 160, 1), (256, 160, 8), (4096, 40, 1)],
+                         ids=lambda g: "P{}_d{}_g{}".format(*g))
+def test_cross_r_only_hint(cuda, geom):
+    """p2p_group.flags GROUP_F_R_ONLY (ABI 14): the host's per-call hint that alpha makes every
+    edit's blend coefficient A zero (a Replace step inside cross_replace_steps, main.py:189), so
+    the dense kernels skip the edits' own Q / K loads and softmax.  With the hint the outputs, the
+    stored maps and the LocalBlend word sums are bit-identical to the unhinted launch; a WRONG hint
+    (alpha 0 on some words: A != 0) falls back inside the kernel and is bit-identical as well."""
+    from p2p_amd import programs
+    P, d, n_groups = geom
+    B, H, K = 4, 8, 77
+    BG = B * n_groups
+    N = 2 * BG
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=6.0, seed=77 + P)
+    scale = d ** -0.5
+    prog = programs.replace_program(_edit_mapper(B, K)).to_device(cuda)
+    lh = 5 * H
+    balpha = torch.rand(B, K, device=cuda, generator=torch.Generator(device=cuda).manual_seed(8))
+
+    def run(alpha, hints):
+        o = torch.empty_like(q)
+        store = torch.zeros(BG * H, P, K, device=cuda)
+        bsums = [torch.zeros(B, 2, lh, P, device=cuda) for _ in range(n_groups)]
+        groups = [(g * B, B, None, None) for g in range(n_groups)]
+        groups += [(BG + g * B, B, prog, alpha, (bsums[g], balpha, None, 0, lh), hints) for g in range(n_groups)]
+        for acc in (False, True):
+            _hip.cross_attn(q, k, v, o, H, scale, groups, store=store, store_slot=[-1] * BG + [i * H for i in range(BG)],
+                            accumulate=acc)
+        return o, store, torch.stack(bsums)
+
+    ones = torch.ones(B - 1, K, device=cuda)
+    mixed = ones.clone()
+    mixed[2, 10:20] = 0.0
+    for alpha in (ones, mixed):
+        plain = run(alpha, 0)
+        hinted = run(alpha, _hip.GROUP_F_R_ONLY)
+        for x, y in zip(plain, hinted):
+            assert torch.equal(x, y), (x.float() - y.float()).abs().max().item()
+    # and the hinted launch is the edit: edit rows' maps equal R = P0 . M_e (alpha 1)
+    o, store, _ = run(ones, _hip.GROUP_F_R_ONLY)
+    p = ref_probs(q, k, H, scale)
+    R = torch.einsum("hpw,bwn->bhpn", p[BG], _edit_mapper(B, K).to(cuda))
+    assert (store[H:B * H] - 2 * R.reshape((B - 1) * H, P, K)).abs().max().item() < 2 * 2e-3

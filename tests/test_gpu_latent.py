@@ -144,3 +144,89 @@ def test_latent_step_builds_folded_blend_mask(cuda, dtype, sub, groups):
     assert torch.equal(got, want), (got - want).abs().max().item()
     with pytest.raises(_hip.HipError):      # out may not alias x in the fused form
         _hip.latent_step(eps, x, x, coeffs, 7.5, None, gs if G > 1 else 0, None, blend)
+
+
+def torch_blend_mask(sums, th_pool, th_sub, size, sub):
+    """null_text.py:41-67 restated in float64 torch on word sums that are already taken
+    (sums [B, 2, L*H, 256]: plane 0 the alpha words, plane 1 the substruct words): mean over the
+    L*H maps, 3x3 max-pool (alpha plane only), nearest upsample, max-normalise, threshold, then
+    mask[:1] + mask, and substruct: mask * ~(sub[:1] + sub).  Returns the mask and, per pixel, the
+    distance of the deciding normalised values from their thresholds."""
+    import torch.nn.functional as F
+
+    def plane(i, pool, th):
+        m = sums[:, i].double().mean(1).reshape(-1, 1, 16, 16)
+        if pool:
+            m = F.max_pool2d(m, (3, 3), (1, 1), padding=(1, 1))
+        m = F.interpolate(m, size=size)
+        m = (m / m.amax(dim=(2, 3), keepdim=True))[:, 0]
+        return m.gt(th), (m - th).abs()
+
+    mask, dist = plane(0, True, th_pool)
+    mask = mask[:1] | mask
+    dist = torch.minimum(dist, dist[:1])
+    if sub:
+        s, sd = plane(1, False, th_sub)
+        mask = mask & ~(s[:1] | s)
+        dist = torch.minimum(dist, torch.minimum(sd, sd[:1]))
+    return mask, dist
+
+
+@pytest.mark.parametrize("sub", [False, True], ids=["nosub", "substruct"])
+def test_folded_blend_mask_matches_torch_restatement(cuda, sub):
+    """The mask builder itself (the wave-per-plane mean and the on-the-fly pooling of
+    build_blend_mask, shared by latent_blend_kernel and blend_finalize_kernel) against a float64
+    torch restatement of null_text.py:41-67 on the same folded word sums: every pixel equal except
+    where a deciding value sits within 1e-5 of its threshold (f32 vs f64 rounding)."""
+    gs, H, L = 4, 8, 5
+    g = torch.Generator(device=cuda).manual_seed(41 + sub)
+    maps = [torch.zeros(gs * H, 256, 77, device=cuda) for _ in range(L)]
+    alpha = torch.ones(gs, 77, device=cuda)
+    subt = torch.ones(gs, 77, device=cuda) if sub else None
+    worst = 0
+    for trial in range(4):
+        base = torch.rand(gs * 2, 1, 4, 4, device=cuda, generator=g) ** 3
+        field = torch.nn.functional.interpolate(base, size=(16, 16), mode="bilinear", align_corners=False)
+        sums = field.reshape(gs, 2, 1, 256) * (0.8 + 0.4 * torch.rand(gs, 2, L * H, 256, device=cuda, generator=g))
+        sums = sums.contiguous()
+        if not sub:
+            sums[:, 1] = 0
+        for th_pool, th_sub in ((0.3, 0.3), (0.5, 0.45)):
+            got = controllers.FoldedBlendMask(maps, H, alpha, subt, th_pool, th_sub, (64, 64), sums).materialize()
+            want, dist = torch_blend_mask(sums, th_pool, th_sub, (64, 64), sub)
+            diff = (got != 0) != want
+            assert 0.05 < want.float().mean().item() < 0.95
+            assert bool((dist[diff] < 1e-5).all()), dist[diff]
+            worst = max(worst, int(diff.sum()))
+    print(f"folded LocalBlend mask vs float64 torch: at most {worst} near-threshold pixels differ")
+    assert worst <= 4
+
+
+@pytest.mark.parametrize("hw", [(63, 63), (64, 62), (12, 12)], ids=["63x63", "64x62", "12x12"])
+def test_latent_step_odd_shapes_fall_back_to_mask_path(cuda, hw):
+    """Latents the one-launch LocalBlend does not take (H*W not a multiple of 4, or smaller than
+    the 16x16 maps) go through p2p_localblend's mask + the mask-reading latent step
+    (ptp_utils._fused_latent_step) instead of failing: the result equals that two-launch path."""
+    from types import SimpleNamespace
+    from p2p_amd import ptp_utils
+    gs, H, L = 4, 8, 5
+    g = torch.Generator(device=cuda).manual_seed(5)
+    maps = [torch.zeros(gs * H, 256, 77, device=cuda) for _ in range(L)]
+    alpha = torch.ones(gs, 77, device=cuda)
+    sums = (0.5 + torch.rand(gs, 2, L * H, 256, device=cuda, generator=g)).contiguous()
+    sums[:, 1] = 0
+    eps = torch.randn(2 * gs, 4, *hw, device=cuda, generator=g)
+    x = torch.randn(gs, 4, *hw, device=cuda, generator=g)
+    s = sched()
+    t = int(s.timesteps[10])
+
+    class Ctrl:
+        def fused_step_mask(self):
+            return True, lambda size: controllers.FoldedBlendMask(maps, H, alpha, None, 0.3, 0.3, size, sums)
+
+    model = SimpleNamespace(scheduler=s)
+    eu, ec = eps.chunk(2)
+    got = ptp_utils._fused_latent_step(model, Ctrl(), eps, eu, ec, x, t, 7.5)
+    mask = controllers.FoldedBlendMask(maps, H, alpha, None, 0.3, 0.3, hw, sums).materialize()
+    want = _hip.latent_step(eps, x, torch.empty_like(x), s.prev_coeffs(t), 7.5, mask)
+    assert torch.equal(got, want)

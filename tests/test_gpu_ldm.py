@@ -13,6 +13,7 @@ import torch
 
 from oracle import control as oc
 from oracle import forward as ofw
+from oracle_runs import EFFECT_BAR, check_effect, check_negative
 from p2p_amd import config, controllers
 from p2p_amd import pipeline as pl
 from p2p_amd import ptp_utils
@@ -22,10 +23,13 @@ pytestmark = pytest.mark.gpu
 GUIDANCE = 7.0
 
 
-def oracle_ldm(model, prompts, x_T, tok, steps):
-    ctrl = oc.OracleController("main", "replace", prompts, steps, 0.8, 0.4, tok)
+def oracle_ldm(model, prompts, x_T, tok, steps, edit=True):
     dev = model.device
-    ctrl.mapper, ctrl.alpha = ctrl.mapper.to(dev), ctrl.alpha.to(dev)
+    if edit:
+        ctrl = oc.OracleController("main", "replace", prompts, steps, 0.8, 0.4, tok)
+        ctrl.mapper, ctrl.alpha = ctrl.mapper.to(dev), ctrl.alpha.to(dev)
+    else:   # the no-edit base of the edit-effect metric (main.py:110-113 EmptyControl)
+        ctrl = oc.OracleController("main", "empty")
     ofw.install(model, ctrl)
     B = len(prompts)
     ids = model.tokenizer(prompts, padding="max_length", max_length=77, return_tensors="pt").input_ids.to(dev)
@@ -43,10 +47,10 @@ def oracle_ldm(model, prompts, x_T, tok, steps):
     return lat, ctrl
 
 
-def product_ldm(model, prompts, x_T, steps, mode, device):
+def product_ldm(model, prompts, x_T, steps, mode, device, edit=True):
     with config.compute_mode(mode):
         ctrl = controllers.AttentionReplace(prompts, steps, cross_replace_steps=0.8, self_replace_steps=0.4,
-                                            device=device)
+                                            device=device) if edit else controllers.EmptyControl()
         lat, _ = ptp_utils.text2image_ldm(model, prompts, ctrl, num_inference_steps=steps,
                                           guidance_scale=GUIDANCE, latent=x_T)
     return lat, ctrl
@@ -66,6 +70,11 @@ def test_ldm_final_latents(cuda, tok, mode, bar):
     cos = cosine(got, want)
     print(f"{mode} final-latent cosine:", [round(c, 7) for c in cos.tolist()])
     assert torch.isfinite(got).all() and cos.min().item() >= bar, cos
+    # the edit's effect against the oracle's no-edit run; the product without the edit must fail it
+    base, _ = oracle_ldm(model, pl.LDM_PROMPTS, x_T, tok, 50, edit=False)
+    check_effect(f"LDM {mode}", got, want, base, EFFECT_BAR)
+    neg, _ = product_ldm(model, pl.LDM_PROMPTS, x_T, 50, mode, cuda, edit=False)
+    check_negative("no edit", neg, want, base, EFFECT_BAR)
 
 
 def test_ldm_store_all_maps(cuda, tok):

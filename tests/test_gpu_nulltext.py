@@ -97,34 +97,45 @@ def test_null_text_inversion_full_schedule(cuda):
     assert worst_u >= 0.999
 
 
-@pytest.mark.parametrize("steps", [4, 16])
-def test_edit_with_null_embeddings(cuda, tok, steps):
+@pytest.mark.parametrize("steps,inner", [(4, 2), (50, 10)], ids=["4x2", "50x10"])
+def test_edit_with_null_embeddings(cuda, tok, steps, inner):
     """configs[4]'s second half: the P2P edit after inversion -- per-step null embeddings (the
     notebook's text2image_ldm_stable(..., uncond_embeddings=...) call; ptp_utils.py:129-172 plus
     the context swap of null_text.py:574-618's caller) + fused AttentionReplace + null_text
     LocalBlend, against the ORACLE run with the SAME null embeddings, latent and weights (eager fp32
-    attention, reference controller semantics, oracle DDIM / LocalBlend).  Bar: final latents
-    cosine >= 0.999 per prompt (north star)."""
+    attention, reference controller semantics, oracle DDIM / LocalBlend).  50x10 is configs[4]'s
+    stated schedule (50 DDIM steps, 10 Adam steps per step, then the 50-step edit).  Bars: final
+    latents cosine >= 0.999 per prompt (north star) and the edit-effect cosine against the
+    oracle's no-edit run with the same embeddings >= 0.99; the same run without the edit must
+    fail it."""
     from oracle import control as oc
-    from oracle_runs import cosine, oracle_controller, oracle_group
+    from oracle_runs import EFFECT_BAR, base_group, check_effect, check_negative, cosine, oracle_controller, \
+        oracle_group
+    from p2p_amd import controllers
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.float32)
     g = torch.Generator().manual_seed(6)
     x0 = torch.randn(1, 4, 64, 64, generator=g).to(cuda)
     prompts = [PROMPT, "a painting of a lion eating a burger"]
     with config.compute_mode("bf16"):
         inv = null_text.NullInversion(model, num_ddim_steps=steps)
-        _, x_T, embs = inv.invert(x0, PROMPT, num_inner_steps=2)
+        _, x_T, embs = inv.invert(x0, PROMPT, num_inner_steps=inner)
         lb = null_text.LocalBlend(prompts, ("squirrel", "lion"), start_blend=0.2, tokenizer=tok, device=cuda)
         ctrl = null_text.AttentionReplace(prompts, steps, 0.8, 0.4, local_blend=lb, tokenizer=tok, device=cuda)
         lat, _ = ptp_utils.text2image_ldm_stable(model, prompts, ctrl, num_inference_steps=steps, latent=x_T,
                                                  uncond_embeddings=embs)
+        neg, _ = ptp_utils.text2image_ldm_stable(model, prompts, controllers.EmptyControl(), num_inference_steps=steps,
+                                                 latent=x_T, uncond_embeddings=embs)
     assert lat.shape == (2, 4, 64, 64) and torch.isfinite(lat).all()
     assert ctrl.cur_step == steps
     # the oracle, same null embeddings (the product's), same x_T
     olb = oc.OracleLocalBlend("null", prompts, ("squirrel", "lion"), tok, start_blend=0.2)
     olb.alpha = olb.alpha.to(cuda)
     octrl = oracle_controller("replace", prompts, tok, steps, cuda, local_blend=olb)
-    want = oracle_group(model, prompts, x_T, octrl, steps, uncond_embeddings=[e.detach() for e in embs])
+    ue = [e.detach() for e in embs]
+    want = oracle_group(model, prompts, x_T, octrl, steps, uncond_embeddings=ue)
     c = cosine(lat, want)
-    print(f"edit after null-text ({steps} steps): final-latent cosine vs oracle {[round(x, 6) for x in c.tolist()]}")
+    print(f"edit after null-text ({steps}x{inner}): final-latent cosine vs oracle {[round(x, 6) for x in c.tolist()]}")
     assert c.min().item() >= 0.999
+    base = base_group(model, prompts, x_T, steps, uncond_embeddings=ue)
+    check_effect(f"edit after null-text ({steps}x{inner})", lat, want, base, EFFECT_BAR)
+    check_negative("no edit", neg, want, base, EFFECT_BAR)

@@ -1,5 +1,8 @@
 """End-to-end parity of a full 50-step edit group (north star: final latents cos >= 0.999,
-LocalBlend masks agreeing on >= 99.9 % of pixels) -- GPU.
+LocalBlend masks agreeing on >= 99.9 % of pixels) -- GPU.  On random-init weights an edit moves the
+latents by ~2 % of their norm, so the absolute cosine is cleared even without any edit; the
+edit-EFFECT cosine (tests/oracle_runs.py: product and oracle displacement from the oracle's
+no-edit run) carries the discrimination, with negative controls that must fail it.
 
 Product: ptp_utils.text2image_ldm_stable with the fused null_text AttentionReplace +
 LocalBlend (bf16 MFMA kernels).  Checker: the same U-Net weights and seed run through the
@@ -12,9 +15,9 @@ import torch
 
 from oracle import control as oc
 from oracle import forward as ofw
-from p2p_amd import config
+from oracle_runs import EFFECT_BAR, base_group, check_effect, check_negative, shifted_replace_mapper
+from p2p_amd import config, controllers
 from p2p_amd import pipeline as pl
-from p2p_amd import ptp_utils
 
 pytestmark = pytest.mark.gpu
 
@@ -60,6 +63,19 @@ def test_edit_group_final_latents(cuda, tok, seed):
     print("final-latent cosine per prompt:", [round(c, 6) for c in cos.tolist()])
     assert torch.isfinite(got).all()
     assert cos.min().item() >= 0.999, cos
+    # the edit's EFFECT: (product - no-edit oracle) along (oracle - no-edit oracle), per edit
+    # prompt -- the absolute cosine above is cleared even by a run without any edit
+    base = base_group(model, prompts, x_T, 50)
+    check_effect("configs[1] f32 U-Net", got, want, base, EFFECT_BAR)
+    # negative controls: the same product run with the edit disabled, and with a wrong mapper
+    with config.compute_mode("bf16"):
+        neg_none = pl.run_edit_group(model, prompts, controllers.EmptyControl(), x_T, num_steps=50)
+        ctrl = pl.make_replace_controller(prompts, 50, device=cuda)
+        ctrl.mapper = shifted_replace_mapper(ctrl.mapper)
+        neg_map = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
+    check_negative("no edit", neg_none, want, base, EFFECT_BAR)
+    check_negative("wrong mapper", neg_map, want, base, EFFECT_BAR)
+    assert cosine(neg_none, want).min().item() >= 0.999     # (what the absolute bar alone would miss)
 
 
 def test_edit_group_check_mode_tight(cuda, tok):

@@ -6,15 +6,17 @@ of the same function runs over gloo in tests/test_distributed.py.
 16 seeds in batches of 8 groups per U-Net call (bf16 U-Net, bf16 kernels, 50 DDIM steps, 1 source
 + 3 AttentionReplace edits + LocalBlend per group).  Two sampled groups -- one from each batch --
 against single-group ORACLE runs on the same weights (fp32 eager attention + reference controller
-+ LocalBlend + DDIM): final latents cosine >= 0.999 per prompt and the gathered 16x16 cross maps
-within 3e-3 (two bf16-U-Net trajectories; test_gpu_bench_config.py); every source prompt's
-gathered map row sums to 1.
++ LocalBlend + DDIM): final latents cosine >= 0.999 per prompt, the edit-effect cosine against the
+oracle's no-edit run >= 0.80 (a no-edit negative control must fail it), and the gathered 16x16
+cross maps within 3e-3 (two bf16-U-Net trajectories; test_gpu_bench_config.py); every source
+prompt's gathered map row sums to 1.
 """
 import pytest
 import torch
 
 from oracle import control as oc
-from oracle_runs import cosine, oracle_controller, oracle_group
+from oracle_runs import (EFFECT_BAR_BF16_UNET, base_group, check_effect, check_negative, cosine, oracle_controller,
+                         oracle_group)
 from p2p_amd import config, controllers, sweep
 from p2p_amd import pipeline as pl
 
@@ -54,3 +56,10 @@ def test_config3_sweep_world1_vs_oracle(cuda, tok):
               f"16x16 map |diff| {dmap:.2e}", flush=True)
         assert cos.min().item() >= 0.999, cos
         assert dmap < 3e-3
+        # the edit's effect against the oracle's no-edit run (bf16 U-Net bar, tests/oracle_runs.py)
+        base = base_group(model, prompts, pl.seed_latent(s), STEPS)
+        check_effect(f"  seed {s}", lat[s], want, base, EFFECT_BAR_BF16_UNET)
+        if s == 3:     # negative control: that seed's group without the edit must fail the bar
+            with config.compute_mode("bf16"):
+                neg = pl.run_edit_group(model, prompts, controllers.EmptyControl(), pl.seed_latent(s), num_steps=STEPS)
+            check_negative("no edit", neg, want, base, EFFECT_BAR_BF16_UNET)

@@ -202,3 +202,36 @@ def test_aggregate_attention_needs_prompt_count_for_plain_store():
     assert out.shape == (16, 16, 77)
     red = pc.reduce_maps(store, 16, ["down"], True, 2)
     assert torch.allclose(red[1], out, atol=1e-6)
+
+
+def test_cross_step_plan(tok):
+    """The per-step cross edit plan (AttentionControlEdit._cross_step) from the host copy of
+    cross_replace_alpha (main.py:189) and the program's c_rep / post: Replace inside the window ->
+    the program with GROUP_F_R_ONLY (A = 0 on every word), past cross_replace_steps -> no program
+    (B = 0, A = 1: P' = P_e exactly); Refine keeps its own probabilities for the new words (A != 0)
+    -> no hint; a per-word window (dict) mixes both -> the plain program."""
+    from p2p_amd import _hip
+    prompts = ["a painting of a squirrel eating a burger", "a painting of a lion eating a burger"]
+    rep = pc.AttentionReplace(prompts, 10, 0.8, 0.4, tokenizer=tok, device=torch.device("cpu"))
+    plans = []
+    for step in range(10):
+        rep.cur_step = step
+        prog, hints = rep._cross_step(torch.device("cpu"), 77)
+        plans.append(("plain" if prog is None else "r_only" if hints == _hip.GROUP_F_R_ONLY else "edit"))
+    assert plans == ["r_only"] * 8 + ["plain"] * 2, plans
+    ref = pc.AttentionRefine(["a photo of a house", "a photo of a big house"], 10, 0.8, 0.4, tokenizer=tok,
+                             device=torch.device("cpu"))
+    ref.cur_step = 0
+    prog, hints = ref._cross_step(torch.device("cpu"), 77)
+    assert prog is not None and hints == 0
+    ref.cur_step = 9
+    assert ref._cross_step(torch.device("cpu"), 77)[0] is None
+    mixed = pc.AttentionReplace(prompts, 10, {"default_": 1.0, "lion": 0.4}, 0.4, tokenizer=tok,
+                                device=torch.device("cpu"))
+    mixed.cur_step = 6          # "lion" past its window, every other word inside
+    prog, hints = mixed._cross_step(torch.device("cpu"), 77)
+    assert prog is not None and hints == 0
+    # the plan follows the alpha table: an in-place change is seen at the next call
+    rep.cur_step = 0
+    rep.cross_replace_alpha.zero_()
+    assert rep._cross_step(torch.device("cpu"), 77)[0] is None

@@ -36,10 +36,10 @@ for step in "$@"; do
     smoke) run 300 "$out/smoke.log" python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$out/smoke.log" ;;
     tests)
       if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
-      run 1100 "$out/tests.log" python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests "${sel[@]}"
+      run 1100 "$out/tests.log" python -u -m pytest -x -v -s --durations=25 --timeout 300 --timeout-method thread -m gpu tests "${sel[@]}"
       tail -1 "$out/tests.log" ;;
     files)
-      run 1100 "$out/files.log" python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu ${arg//,/ }
+      run 1100 "$out/files.log" python -u -m pytest -x -v -s --durations=15 --timeout 300 --timeout-method thread -m gpu ${arg//,/ }
       tail -1 "$out/files.log" ;;
     ab)
       for v in ${arg//,/ }; do
