@@ -132,7 +132,13 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
       *reinterpret_cast<short8_t*>(Ks + (i / PC) * KS + D + 8 * (i % PC)) = short8_t{};
   }
   // (V and mapper rows K..KR: the staging writes the zeros its range-checked loads return; V
-  // columns D..DV are only read into O^T rows >= D, which are never stored)
+  // columns D+1..DV are only read into O^T rows > D, which are never stored).  V column D is 1 on
+  // the K key rows and 0 past them, so O^T row D is the row sum of the bf16 weights P V used: the
+  // plain entries take that sum instead of an f32 sum and a normalised P (the staging never
+  // writes column D, so this holds for every entry)
+  constexpr bool kOnesCol = DV > D;   // (d = 160, experiments builds only: no padding column)
+  if constexpr (kOnesCol)
+    for (int r = tid; r < KR; r += NT) Vs[r * VS + D] = r < K ? (uint16_t)0x3F80 : (uint16_t)0;
 
   // ---- the pipelined entry loads: K / V chunks, mapper chunks, coefficients, blend weights, Q
   short8_t kreg[NCH], vreg[NCH];
@@ -269,6 +275,9 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     const bool is_edit = EDIT && edits && b > 0;
     const bool need_own = !is_edit || (eflags & 1);
     const bool need_r = is_edit && (eflags & 2);
+    // a plain entry (no edit, not the source the edits read, maps not kept): unnormalised P
+    // through P V, O scaled by 1 / (O^T row D) once (the per-entry kernel's lean path)
+    const bool lean = kOnesCol && !is_edit && !(edits && b == 0) && !stored;
 
     // ---- P_e = softmax(c K_e Q_e^T), exact, f32 (an edit whose blend reads only R skips it)
     float sv[KB][16];
@@ -303,6 +312,14 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
         for (int r = 0; r < 16; ++r)
           if (!(kShort && kb == KB - 1 && r >= 8)) mx = fmaxf(mx, sv[kb][r]);
       mx = fmaxf(mx, other_half(mx)) * c;
+      if (lean) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            sv[kb][r] = (kShort && kb == KB - 1 && r >= 8) ? 0.f : fast_exp2(fmaf(sv[kb][r], c, -mx));
+        return;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
@@ -436,6 +453,11 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MmaBf16{}, O, Vs, kb * 32, sv[kb], lane);
+    // O^T row D (d tile D / 32, register kLr of lane half kLh): the row sum of a lean entry
+    constexpr int kLrr = D % 32;
+    constexpr int kLh = (kLrr >> 2) & 1;
+    constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
+    const float inv = lean ? 1.f / __shfl(O[kOnesCol ? D / 32 : 0][kLr], (lane & 31) + 32 * kLh) : 1.f;
     if (prow) {
       uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)e * a.bso + h * D + (int64_t)p * a.ldo;
 #pragma unroll
@@ -443,7 +465,8 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int dd = dt * 32 + 8 * g + 4 * hh;
-          if (dd < D) store4(op + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2], O[dt][4 * g + 3]);
+          if (dd < D)
+            store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv, O[dt][4 * g + 3] * inv);
         }
     }
     P2P_GROUP_STAMP(5 + 5 * b)

@@ -95,9 +95,10 @@ def seed_latent(seed: int) -> torch.Tensor:
 
 def make_replace_controller(prompts: Sequence[str], num_steps: int = 50, cross_replace_steps=0.8,
                             self_replace_steps=0.4, blend_words=BLEND_WORDS, store_self_maps=False,
-                            device=None):
+                            device=None, blend_th=(.3, .3)):
     from . import null_text
-    lb = null_text.LocalBlend(list(prompts), blend_words, device=device) if blend_words is not None else None
+    lb = (null_text.LocalBlend(list(prompts), blend_words, th=blend_th, device=device)
+          if blend_words is not None else None)
     ctrl = null_text.AttentionReplace(list(prompts), num_steps, cross_replace_steps=cross_replace_steps,
                                       self_replace_steps=self_replace_steps, local_blend=lb, device=device)
     ctrl.store_self_maps = store_self_maps

@@ -12,6 +12,13 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# MIOpen's default find mode benchmarks every convolution solver (naive ones included) the first
+# time a shape is seen -- on a fresh GPU box that is minutes per U-Net batch size and dtype.  The
+# tests compare product and oracle runs of the SAME U-Net in one process, so which solver MIOpen
+# picks does not matter to them; FAST picks one from its heuristics at once.  (bench.py keeps the
+# default: its warmup groups absorb the search.)
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")

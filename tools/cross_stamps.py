@@ -21,13 +21,13 @@ NWG, W, SLOTS = 4096, 4, 24
 PLAIN = [(0, 1, "loads issued"), (1, 2, "LDS staged + barrier"), (2, 3, "QK + softmax"), (3, 4, "PV"),
          (4, 5, "O store")]
 EDIT = [(0, 19, "  (dense) loads issued"), (19, 20, "  (dense) mapper landed"), (20, 21, "  (dense) coeffs"),
-        (21, 22, "  (dense) K_src landed"), (22, 8, "  (dense) barrier"), (0, 8, "src stage + barrier"), (8, 9, "P0"), (9, 10, "R = P0 M + barrier"), (10, 11, "own stage + barrier"),
+        (21, 22, "  (dense) K_src landed"), (22, 8, "  (dense) barrier"), (0, 8, "src stage + barrier"), (0, 11, "start -> own softmax"), (8, 9, "P0"), (9, 10, "R = P0 M + barrier"), (10, 11, "own stage + barrier"),
         (11, 12, "own QK + softmax"), (12, 13, "blend"), (13, 14, "store epilogue"), (14, 15, "PV"),
         (13, 16, "  store: sync + slab write"), (16, 17, "  store: sync"), (17, 18, "  store: blend sums"),
         (18, 14, "  store: read-add-write")]
 
 
-def run(name, P, d, store, blend):
+def run(name, P, d, store, blend, hint=0):
     N, H, K, B = 8, 8, 77, 4
     C = H * d
     tok = default_tokenizer()
@@ -40,10 +40,10 @@ def run(name, P, d, store, blend):
     o = torch.empty_like(q)
     st = torch.zeros(B * H, P, K, device="cuda") if store else None
     slots = [-1] * B + [i * H for i in range(B)] if store else None
-    grp = [(0, B, None, None), (B, B, prog, alpha)]
+    grp = [(0, B, None, None), (B, B, prog, alpha, None, hint)]
     if blend:
         grp[1] = (B, B, prog, alpha, (torch.zeros(B, 2, 5 * H, P, device="cuda"), torch.rand(B, K, device="cuda"),
-                                      None, 0, 5 * H))
+                                      None, 0, 5 * H), hint)
     fn = _hip.lib().p2p_diag_cross_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     for _ in range(10):
@@ -84,6 +84,8 @@ def run(name, P, d, store, blend):
 
 
 if __name__ == "__main__":
-    run("G1", 4096, 40, False, False)
     run("G2", 1024, 80, True, False)
+    run("G2 R_ONLY", 1024, 80, True, False, _hip.GROUP_F_R_ONLY)
     run("G3", 256, 160, True, True)
+    run("G3 R_ONLY", 256, 160, True, True, _hip.GROUP_F_R_ONLY)
+    run("G4 R_ONLY", 64, 160, True, False, _hip.GROUP_F_R_ONLY)
