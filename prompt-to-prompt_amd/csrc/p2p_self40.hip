@@ -672,13 +672,18 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
   if (d == 80) {
     switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
-      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);        // round 3's pinned schedule
-      case 164: return (int)launch<80, 4, 2, 128, false, 1 | 16>(a, st);  // default with clock stamps
+      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);        // round 3's default
+      case 110: return (int)launch<80, 4, 2, 128, false, 1>(a, st);      // round 4's default
+      case 102: return (int)launch<80, 8, 1, 128, false, 1>(a, st);
+      case 164: return (int)launch<80, 8, 1, 128, true, 1 | 128 | 256 | 512 | 16384 | 16>(a, st);  // default + stamps
 #endif
-      // d = 80 (one wave per SIMD): the compiler's own schedule (no sched_group_barrier pinning)
-      // measured 0.0269 vs 0.0277-0.0278 ms at G2 (profiles/r04/ab_d80_r04f.log; variant 92 is the
-      // pinned schedule, round 3's default)
-      default: return (int)launch<80, 4, 2, 128, false, 1>(a, st);
+      // d = 80: 8 waves x ONE 32-row query block (two waves per SIMD), 128-key tiles, split staging
+      // and the younger half's priority duty of the d = 40 kernel.  In the pipeline (bench.py,
+      // HIP events) 36.8-37.2 -> 30.9-31.2 us against round 4's 4 waves x 2 blocks (one wave per
+      // SIMD), which is as fast only with hot inputs: the second wave hides the cold Q / K / V
+      // loads the layer meets after its QKV GEMM (profiles/r05/d80_ab/; 4 x 1 x 64: 34.0, 8 x 1 x
+      // 64: 35.9, without split staging or priority: 32.0-33.0)
+      default: return (int)launch<80, 8, 1, 128, true, 1 | 128 | 256 | 512 | 16384>(a, st);
     }
   }
   switch (a.variant) {
@@ -686,6 +691,11 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 163: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 16>(a, st);   // default with clock stamps
 #endif
     case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
+#ifdef P2P_EXPERIMENTS
+    // in-pipeline A/B (round 5): 128-key tiles (78 KB of LDS: two workgroups per CU)
+    case 170: return (int)launch<40, 8, 2, 128, true, 1 | 128 | 256 | 512 | 16384 | 8388608>(a, st);
+    case 171: return (int)launch<40, 8, 1, 256, true, 1 | 128 | 256 | 512 | 16384 | 8388608>(a, st);
+#endif
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // three of every four steps (round 3: 0.1867 ms vs 0.1880-0.1885 for priority on alternate step
     // pairs and 0.2056 for round 2, profiles/r03/g1_ab/r03y_ab.log), and K's f16 range check as a
