@@ -26,7 +26,9 @@ def main(iters=20, mode="edit", P=4096, d=40):
     o = torch.empty_like(q)
     store = torch.zeros(B * H, P, K, device="cuda") if "store" in mode else None
     slots = [-1] * B + [i * H for i in range(B)]
-    grp = [(0, B, None, None), (B, B, prog if "edit" in mode else None, alpha if "edit" in mode else None)]
+    # (edit modes carry the R_ONLY hint, as the controllers pass it inside cross_replace_steps)
+    grp = [(0, B, None, None), (B, B, prog if "edit" in mode else None, alpha if "edit" in mode else None, None,
+                                _hip.GROUP_F_R_ONLY if "edit" in mode else 0)]
     for _ in range(iters):
         _hip.cross_attn(q, k, v, o, H, d ** -0.5, grp, store=store,
                         store_slot=slots if store is not None else None, accumulate=store is not None)
