@@ -1322,8 +1322,8 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       if (tid < 2 * K) btab[tid < K ? 0 : 1][tid < K ? tid : tid - K] = bw0;
       if (i1 < 2 * K) btab[i1 < K ? 0 : 1][i1 < K ? i1 : i1 - K] = bw1;
       // columns K.. of both tables are zero (the 16-byte weight reads of the register sums)
-      for (int i = tid; i < 2 * (P2P_MAX_KEYS_CROSS - K); i += NT)
-        btab[i / (P2P_MAX_KEYS_CROSS - K)][K + i % (P2P_MAX_KEYS_CROSS - K)] = 0.f;
+      static_assert(P2P_MAX_KEYS_CROSS <= NT, "one padding column per thread");
+      if (tid < P2P_MAX_KEYS_CROSS - K) btab[0][K + tid] = btab[1][K + tid] = 0.f;
     }
     if (touch_when == 0) touch();
   };
@@ -1684,13 +1684,22 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // key blocks wholly below K write every register (one branch per block, wave-uniform); only
+    // the block that crosses K checks its keys (a per-element check costs a compare and two exec
+    // updates around every LDS write)
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb) {
+      if (kb * 32 + 32 <= K) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int w = kb * 32 + acc_row(r, hh);
-        if (w < K) slab[qi * K + w] = sv[kb][r];
+        for (int r = 0; r < 16; ++r) slab[qi * K + kb * 32 + acc_row(r, hh)] = sv[kb][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int w = kb * 32 + acc_row(r, hh);
+          if (w < K) slab[qi * K + w] = sv[kb][r];
+        }
       }
+    }
     P2P_CROSS_STAMP(16)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1705,20 +1714,21 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     // deviation from the map path; the sequential chain cost ~3k cycles per workgroup.)
     if (blend_on) {
       const bool has_sub = a.grp_bsub[gi] != nullptr;
+      // (no key checks: past K both the probabilities -- masked to exact zeros by every path --
+      // and the weights are 0, so those terms add +0; runs past the short tail are skipped)
       float sa = 0.f, ss = 0.f;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
+          if (kb == KB - 1 && g4 >= 2 && short_tail) continue;   // registers 8..15: keys >= 80
           const int w0 = kb * 32 + 8 * g4 + 4 * hh;
-          if (w0 >= K) continue;   // (btab is zero past K: the run that straddles K adds zeros)
           const f32x4_t ta = *reinterpret_cast<const f32x4_t*>(&btab[0][w0]);
           const f32x4_t ts = *reinterpret_cast<const f32x4_t*>(&btab[1][w0]);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float pv = w0 + j < K ? sv[kb][4 * g4 + j] : 0.f;
-            sa = fmaf(pv, ta[j], sa);
-            ss = fmaf(pv, ts[j], ss);
+            sa = fmaf(sv[kb][4 * g4 + j], ta[j], sa);
+            ss = fmaf(sv[kb][4 * g4 + j], ts[j], ss);
           }
         }
       sa += other_half(sa);

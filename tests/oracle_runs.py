@@ -92,12 +92,14 @@ def edit_effect(got, want, base, first_edit=1):
 
 # The edit-effect bars.  f32 U-Net (both trajectories see the same activations up to the
 # attention's own rounding): 0.99.  bf16 U-Net (two bf16 trajectories whose activations round
-# differently, ~0.8 % of the latent norm against an edit of ~2 %): 0.80 on the random-init
-# weights, 0.99 once the maps are sharpened (gain 4: the edit moves ~14 %).  Every negative
-# control (no edit, a wrong mapper, no reweight, a wrong refine gather) measured <= 0.70 at every
-# precision and gain (tools/effect_probe.py, profiles/r05/effect_probe.log).
+# differently, ~0.8 % of the latent norm against an edit of ~2 %): 0.70 on the random-init
+# weights (measured 0.81-0.95 over seeds and boxes; every negative control <= 0.45 there), 0.99
+# once the maps are sharpened (gain 4: the edit moves ~14 %).  Every negative control (no edit, a
+# wrong mapper, no reweight, a wrong refine gather) measured <= 0.64 at every precision and gain
+# but LocalBlend-off on partial masks (<= 0.84; bar 0.97 there) -- tools/effect_probe.py,
+# profiles/r05/effect_probe.log and the r05 GPU test logs.
 EFFECT_BAR = 0.99
-EFFECT_BAR_BF16_UNET = 0.80
+EFFECT_BAR_BF16_UNET = 0.70
 
 
 def check_effect(label, got, want, base, bar, first_edit=1):

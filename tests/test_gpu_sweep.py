@@ -7,7 +7,7 @@ of the same function runs over gloo in tests/test_distributed.py.
 + 3 AttentionReplace edits + LocalBlend per group).  Two sampled groups -- one from each batch --
 against single-group ORACLE runs on the same weights (fp32 eager attention + reference controller
 + LocalBlend + DDIM): final latents cosine >= 0.999 per prompt, the edit-effect cosine against the
-oracle's no-edit run >= 0.80 (a no-edit negative control must fail it), and the gathered 16x16
+oracle's no-edit run >= 0.70 (a no-edit negative control must fail it), and the gathered 16x16
 cross maps within 3e-3 (two bf16-U-Net trajectories; test_gpu_bench_config.py); every source
 prompt's gathered map row sums to 1.
 """
