@@ -376,7 +376,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} launched with WORLD_SIZE={world}")
-    if world > 1:
+    # every rank torchrun starts joins an RCCL process group -- world 1 included, so a one-GPU box
+    # runs the same init / barrier / all-gather / all-reduce path the 8-GPU node does
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -408,7 +411,7 @@ def main():
         warm_seeds = [10 ** 6 + rank * args.warmup * G + i for i in range(args.warmup * G)]
     for i in range(args.warmup):
         batch(warm_seeds[i * G:(i + 1) * G])
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timer.enabled = True
@@ -427,11 +430,11 @@ def main():
     lat_all, maps_all = sweep.run_batched_sweep(all_seeds, batch, batch.out_shapes, rank, world, G,
                                                 device=dev, on_batch=progress)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timer.enabled = False
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
@@ -489,7 +492,7 @@ def main():
             "roofline_hbm": timer.hbm_lines(),
         }
         print(json.dumps(line))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -6,7 +6,8 @@ source's probabilities inside the attention kernel -- so the sweep shards whole 
 across ranks (round-robin by seed, weak scaling) with no collective on the data path, and
 gathers each group's results once at the end: the final latents AND the reduced stored maps
 (aggregate_attention's 16x16 cross maps per prompt, main.py:293-307), packed into ONE
-all-gather (RCCL over xGMI on GPUs, gloo on CPU).
+all-gather (RCCL over xGMI on GPUs, gloo on CPU).  Inside a process group the gather runs even at
+world size 1 (torchrun with one rank: the same collective path as the 8-GPU node).
 """
 from __future__ import annotations
 
@@ -18,6 +19,10 @@ import torch.distributed as dist
 Result = Union[torch.Tensor, Tuple[torch.Tensor, ...]]
 
 
+def _in_group() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def partition(seeds: Sequence[int], rank: int, world: int) -> List[int]:
     """Round-robin shard: rank r gets seeds[r], seeds[r + world], ..."""
     return list(seeds[rank::world])
@@ -26,7 +31,7 @@ def partition(seeds: Sequence[int], rank: int, world: int) -> List[int]:
 def gather_latents(local: torch.Tensor, n_total: int, world: int) -> torch.Tensor:
     """All-gather per-rank stacks [n_local, ...] (ranks may hold one group fewer) and return
     them in global seed order [n_total, ...]."""
-    if world == 1:
+    if world == 1 and not _in_group():
         return local
     per = (n_total + world - 1) // world
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
@@ -47,7 +52,7 @@ def gather_results(local: Sequence[torch.Tensor], n_total: int, world: int) -> L
     n_local = local[0].shape[0]
     if any(t.shape[0] != n_local for t in local):
         raise ValueError("every result needs one row per local group")
-    if world == 1:
+    if world == 1 and not _in_group():
         return list(local)
     widths = [int(t[0].numel()) if n_local else int(torch.Size(t.shape[1:]).numel()) for t in local]
     packed = torch.cat([t.reshape(n_local, w) for t, w in zip(local, widths)], dim=1)

@@ -63,3 +63,30 @@ def test_config3_sweep_world1_vs_oracle(cuda, tok):
             with config.compute_mode("bf16"):
                 neg = pl.run_edit_group(model, prompts, controllers.EmptyControl(), pl.seed_latent(s), num_steps=STEPS)
             check_negative("no edit", neg, want, base, EFFECT_BAR_BF16_UNET)
+
+
+def test_bench_under_torchrun_world1_rccl(cuda):
+    """bench.py as the driver launches it on a node (torch.distributed.run, one rank per GPU), with
+    ONE rank on this box's GPU: the RCCL process group init, barriers, the packed all-gather of
+    the final latents + maps and the max-over-ranks all-reduce all run on hardware (at world 1 the
+    collectives are identities, but the nccl path is the one the 8-GPU scaling run takes).  2 DDIM
+    steps per group keep it short."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--ddim-steps", "2", "--no-cpu-baseline"]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print("torchrun world-1 bench:", line["value"], "edit-groups/s at 2 DDIM steps", flush=True)
+    assert line["n_gpus"] == 1 and line["config"]["groups_total"] == 2 and line["value"] > 0

@@ -45,7 +45,7 @@ def run(name, P, d, store):
     o = torch.empty_like(q)
     st = torch.zeros(B * H, P, K, device="cuda") if store else None
     slots = [-1] * B + [i * H for i in range(B)] if store else None
-    grp = [(0, B, None, None), (B, B, prog, alpha)]
+    grp = [(0, B, None, None), (B, B, prog, alpha, None, _hip.GROUP_F_R_ONLY)]   # (alpha 1: the hint)
     fn = _hip.lib().p2p_diag_group_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     for _ in range(10):
@@ -84,4 +84,3 @@ def run(name, P, d, store):
 
 if __name__ == "__main__":
     run("G1", 4096, 40, False)
-    run("G2", 1024, 80, True)
