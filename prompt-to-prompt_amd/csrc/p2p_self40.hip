@@ -691,15 +691,6 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
     case 163: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 16>(a, st);   // default with clock stamps
 #endif
     case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
-#ifdef P2P_EXPERIMENTS
-    // in-pipeline A/B (round 5): 128-key tiles (78 KB of LDS: two workgroups per CU)
-    case 170: return (int)launch<40, 8, 2, 128, true, 1 | 128 | 256 | 512 | 16384 | 8388608>(a, st);
-    case 171: return (int)launch<40, 8, 1, 256, true, 1 | 128 | 256 | 512 | 16384 | 8388608>(a, st);
-    // the priority duty in the pipeline: none / alternate step pairs / 2 of every 4 steps
-    case 172: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 8388608>(a, st);
-    case 173: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 8388608>(a, st);
-    case 174: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 8388608>(a, st);
-#endif
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
     // three of every four steps (round 3: 0.1867 ms vs 0.1880-0.1885 for priority on alternate step
     // pairs and 0.2056 for round 2, profiles/r03/g1_ab/r03y_ab.log), and K's f16 range check as a

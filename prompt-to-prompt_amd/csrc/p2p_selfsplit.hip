@@ -348,9 +348,6 @@ bool self_ring_eligible(const SelfArgs& a, int d) {
 
 int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
   (void)d;
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 135) return (int)launch_ring<2>(a, st);   // in-pipeline A/B (round 5)
-#endif
   return (int)launch_ring<4>(a, st);
 }
 
