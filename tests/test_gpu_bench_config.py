@@ -105,13 +105,14 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
     # north star: >= 99.9 % of the pixels at EVERY step where both sides see the same maps.  Across
     # the two bf16 trajectories a partial mask (coverage < 1, the sharpened run) moves by whole 4x4
     # blocks of the 16x16 maps wherever a map value sits near its threshold, so there the run-vs-run
-    # agreement is held to 99 % on average and 95 % per step (all-ones masks: 99.9 % every step)
+    # agreement is held to 98 % on average and 95 % per step (measured 99.3 % / 96.9 %; all-ones
+    # masks: 99.9 % every step)
     print("  per-step agreement vs the oracle's run:", [round(x, 4) for x in agree])
     assert min(forced) >= 0.999, forced
     if min(cover) == 1.0:
         assert min(agree) >= 0.999, agree
     else:
-        assert sum(agree) / n >= 0.99 and min(agree) >= 0.95, agree
+        assert sum(agree) / n >= 0.98 and min(agree) >= 0.95, agree
     # the edit's effect, and negative controls that must fail the same bar
     base = base_group(model, prompts, x_T, 50)
     check_effect(f"configs[1] as benched, gain {gain}", got, want, base, effect_bar)
