@@ -1057,7 +1057,9 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #define P2P_CROSS_STAMP(i)
 #endif
 
-template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
+// LEGACY (experiments A/B only): round 5's first staging -- a branch around every Q / K / V load,
+// the wave's row base in a VGPR
+template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE, bool LEGACY = false>
 __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -1126,7 +1128,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // cross_replace_steps, main.py:189), so P' = R B: the entry's own Q K^T softmax is not needed and
   // neither are its Q and K -- only its V (checked again from the coefficients below)
   const bool r_only = (info >> 18) & 1;
-  const int p0w = qt * 32 * WAVES + wave * 32;
+  // wave-uniform in a scalar register: the buffer resources built from it (Q rows, the running-sum
+  // rows) stay scalar -- from a VGPR every such load became a readfirstlane waterfall loop
+  const int p0w = LEGACY ? qt * 32 * WAVES + wave * 32 : __builtin_amdgcn_readfirstlane(qt * 32 * WAVES + wave * 32);
   const int p = p0w + qi;
   const bool prow = p < a.P;
   const int K = a.K;
@@ -1340,12 +1344,27 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   }
   for (int i = tid; i < (KR - K) * VS; i += NT) Vs[K * VS + i] = EV(0);
 
+  // bf16 inputs: Q rows and K / V chunks by range-checked buffer loads issued unconditionally
+  // (rows >= P / >= K read as zeros).  Loads inside a branch per fragment or chunk made hipcc
+  // re-load kernel arguments and drain the earlier loads with vmcnt(0) between them: the stored
+  // source / plain entries' staging ran as a chain of round trips
+  constexpr bool kBufIO = !LEGACY && std::is_same<IO, uint16_t>::value && std::is_same<MQ, QkBf16<uint16_t>>::value;
   auto load_q = [&](int e, typename MQ::frag (&qf)[NKT]) {
     const IO* qp = static_cast<const IO*>(a.q) + (int64_t)e * a.bsq + h * D;
+    if constexpr (kBufIO) {
+      const __amdgpu_buffer_rsrc_t rq = make_rsrc(qp + (int64_t)p0w * a.ldq, ((int64_t)(a.P - 1 - p0w) * a.ldq + D) * 2);
 #pragma unroll
-    for (int t = 0; t < NKT; ++t) {
-      const int col = 16 * t + 8 * hh;
-      qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+      for (int t = 0; t < NKT; ++t) {
+        const int col = 16 * t + 8 * hh;
+        qf[t].h = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rq, (qi * (int)a.ldq + col) * 2, 0, 0));
+        if (col >= D) qf[t] = MQ::zero();
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) {
+        const int col = 16 * t + 8 * hh;
+        qf[t] = (prow && col < D) ? MQ::load_q(qp + (int64_t)p * a.ldq + col) : MQ::zero();
+      }
     }
   };
 
@@ -1354,6 +1373,19 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   auto load_kv = [&](int e, Chunk8<IO> (&kc)[NCH], Chunk8<IO> (&vc)[NCH], bool withV, bool withK = true) {
     const IO* kp = static_cast<const IO*>(a.k) + (int64_t)e * a.bsk + h * D;
     const IO* vp = static_cast<const IO*>(a.v) + (int64_t)e * a.bsv + h * D;
+    if constexpr (kBufIO) {
+      const __amdgpu_buffer_rsrc_t rk = make_rsrc(kp, ((int64_t)(K - 1) * a.ldk + D) * 2);
+      const __amdgpu_buffer_rsrc_t rv = make_rsrc(vp, ((int64_t)(K - 1) * a.ldv + D) * 2);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int cidx = tid + i * NT;
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        if (withK) kc[i].load_buf(rk, (uint32_t)((row * (int)a.ldk + ch * 8) * 2));
+        if (withV) vc[i].load_buf(rv, (uint32_t)((row * (int)a.ldv + ch * 8) * 2));
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
@@ -1371,7 +1403,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
-      if (cidx < K * CPR) {
+      if (cidx < K * CPR) {   // (V rows K..KR are zeroed with the padding; K rows past K are masked)
         if (withK) MQ::stage(kc[i], Ks + row * KS + ch * 8, KPLANE);
         if (withV) vc[i].store(Vs + row * VS + ch * 8);
       }
@@ -1874,6 +1906,13 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 191) {
+    if (dense) hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, true>), grid, block, dyn, st, b);
+    else hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false, true>), grid, block, dyn, st, b);
+    return hipGetLastError();
+  }
+#endif
   if (dense)
     hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
   else

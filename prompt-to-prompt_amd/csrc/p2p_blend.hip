@@ -112,7 +112,9 @@ __device__ __forceinline__ void build_blend_mask(const float* ws0, const float* 
   // four adjacent map pixels, so every load is one 16-byte row piece and a wave's LH loads of a
   // plane are all in flight at once (one memory round trip for the whole mask)
   {
-    const int g = tid >> 6, k = g & 1, sidx = g >> 1;     // (source | b) x (alpha | substruct)
+    // (source | b) x (alpha | substruct); the wave index in a scalar register, so the plane's buffer
+    // resource is scalar too (from a VGPR each of the 48 loads became a readfirstlane waterfall loop)
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6), k = g & 1, sidx = g >> 1;
     const int px0 = (tid & 63) * 4;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (px0 < R2 && (sidx == 0 || sub)) {

@@ -118,7 +118,9 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   const int K = a.K;
   const int P = a.P;
   const float c = a.scale_log2;
-  const int p0w = qt * 32 * W + wave * 32;
+  // wave-uniform in a scalar register (the running-sum buffer resources built from it stay scalar:
+  // from a VGPR each of their loads was a readfirstlane waterfall loop)
+  const int p0w = __builtin_amdgcn_readfirstlane(qt * 32 * W + wave * 32);
   const int p = p0w + qi;
   const bool prow = p < P;
   float* const slab = reinterpret_cast<float*>(cross_dyn) + wave * 32 * K;
