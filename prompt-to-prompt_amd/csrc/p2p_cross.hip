@@ -48,8 +48,10 @@ constexpr int group_occupancy() {
   return (D <= 40 && !(EDIT && STORE)) || (D <= 80 && !EDIT && !STORE) ? 2 : 1;
 }
 
-template <int D, int W, bool EDIT, bool STORE>
+// LEGACY (experiments A/B only): the key mask by per-register compares, no mask column
+template <int D, int W, bool EDIT, bool STORE, bool LEGACY = false>
 __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
+  constexpr bool kMaskCol = !LEGACY && (D + 15) / 16 * 16 > D;   // K column D carries the key mask
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   constexpr int NKT = DK / 16;
@@ -128,10 +130,17 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
 
   // ---- padding the MFMAs read and the staging never writes (written once; the staging writes
   // columns < D): K columns D..DK (met by Q's zero columns)
+  // K column D carries the key mask: -2^100 (bf16 0xF180) on the rows past K, 0 below, met by a 1 in
+  // every Q row's column D, so a masked key's logit leaves the MFMA at -2^100 (below any real logit,
+  // exp -> 0 exactly) and no per-register compare is needed (the rows' columns < D are the zeros the
+  // staging loads return)
   if constexpr (DK > D) {
     constexpr int PC = (DK - D) / 8;
-    for (int i = tid; i < KR * PC; i += NT)
-      *reinterpret_cast<short8_t*>(Ks + (i / PC) * KS + D + 8 * (i % PC)) = short8_t{};
+    for (int i = tid; i < KR * PC; i += NT) {
+      const int row = i / PC, j = i % PC;
+      *reinterpret_cast<short8_t*>(Ks + row * KS + D + 8 * j) =
+          short8_t{(short)(kMaskCol && j == 0 && row >= K ? 0xF180 : 0), 0, 0, 0, 0, 0, 0, 0};
+    }
   }
   // (V and mapper rows K..KR: the staging writes the zeros its range-checked loads return; V
   // columns D+1..DV are only read into O^T rows > D, which are never stored).  V column D is 1 on
@@ -258,7 +267,9 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     const int eflags = next_flags;   // workgroup-uniform
     short8_t qc[NKT];   // this entry's Q rows (qf is refilled for the next entry below)
 #pragma unroll
-    for (int t = 0; t < NKT; ++t) qc[t] = (16 * t + 8 * hh < D) ? qf[t] : short8_t{};   // columns >= D: 0
+    for (int t = 0; t < NKT; ++t)   // columns >= D: 0, but column D = 1 (the key-mask column)
+      qc[t] = (16 * t + 8 * hh < D) ? qf[t]
+                                    : (kMaskCol && 16 * t + 8 * hh == D ? short8_t{0x3F80, 0, 0, 0, 0, 0, 0, 0} : short8_t{});
     const bool more = b + 1 < count;
     if (more) load_entry(b + 1);   // lands while this entry computes
     const bool stored = STORE && a.store_slot[e] >= 0;
@@ -299,10 +310,14 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[kb][r] = acc[r];
-      if (kb * 32 + 32 > K) {   // wave-uniform: only the block that runs past K
+      if (!kMaskCol && kb * 32 + 32 > K) {   // (no mask column) wave-uniform: only the block past K
+        // K made opaque per entry: hoisted out of the entry loop, the 16 per-register lane masks
+        // were spilled to VGPR lanes and each restored by two v_readlane (plus a hazard s_nop)
+        int Kl = K - kb * 32;
+        if constexpr (!LEGACY) asm volatile("" : "+s"(Kl));
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (kb * 32 + acc_row(r, hh) >= K) sv[kb][r] = -INFINITY;
+          if (acc_row(r, hh) >= Kl) sv[kb][r] = -INFINITY;
       }
     }
     auto soft = [&](auto tail) __attribute__((always_inline)) {
@@ -491,7 +506,7 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   }
 }
 
-template <int D, int W>
+template <int D, int W, bool LEGACY = false>
 hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   CrossArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
@@ -499,10 +514,10 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   const bool store = a.any_store != 0;
   const size_t dyn = store ? (size_t)W * 32 * a.K * sizeof(float) : 0;
   dim3 grid(b.n_qtiles * a.H * a.n_groups), block(64 * W);
-  if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
-  else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
-  else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
-  else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false>), grid, block, dyn, st, b);
+  if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true, LEGACY>), grid, block, dyn, st, b);
+  else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false, LEGACY>), grid, block, dyn, st, b);
+  else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true, LEGACY>), grid, block, dyn, st, b);
+  else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false, LEGACY>), grid, block, dyn, st, b);
   return hipGetLastError();
 }
 
@@ -532,7 +547,7 @@ bool cross_group_eligible(const CrossArgs& a, int d) {
 int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
 #ifdef P2P_EXPERIMENTS
-    case 40: return (int)launch_group<40, 4>(a, st);
+    case 40: return a.variant == 192 ? (int)launch_group<40, 4, true>(a, st) : (int)launch_group<40, 4>(a, st);
     case 80: return (int)launch_group<80, 4>(a, st);
     case 160: return (int)launch_group<160, 4>(a, st);
 #else
