@@ -1057,9 +1057,7 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #define P2P_CROSS_STAMP(i)
 #endif
 
-// LEGACY (experiments A/B only): round 5's first staging -- a branch around every Q / K / V load,
-// the wave's row base in a VGPR
-template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE, bool LEGACY = false>
+template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
 __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -1130,7 +1128,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   const bool r_only = (info >> 18) & 1;
   // wave-uniform in a scalar register: the buffer resources built from it (Q rows, the running-sum
   // rows) stay scalar -- from a VGPR every such load became a readfirstlane waterfall loop
-  const int p0w = LEGACY ? qt * 32 * WAVES + wave * 32 : __builtin_amdgcn_readfirstlane(qt * 32 * WAVES + wave * 32);
+  const int p0w = __builtin_amdgcn_readfirstlane(qt * 32 * WAVES + wave * 32);
   const int p = p0w + qi;
   const bool prow = p < a.P;
   const int K = a.K;
@@ -1348,7 +1346,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // (rows >= P / >= K read as zeros).  Loads inside a branch per fragment or chunk made hipcc
   // re-load kernel arguments and drain the earlier loads with vmcnt(0) between them: the stored
   // source / plain entries' staging ran as a chain of round trips
-  constexpr bool kBufIO = !LEGACY && std::is_same<IO, uint16_t>::value && std::is_same<MQ, QkBf16<uint16_t>>::value;
+  constexpr bool kBufIO = std::is_same<IO, uint16_t>::value && std::is_same<MQ, QkBf16<uint16_t>>::value;
   auto load_q = [&](int e, typename MQ::frag (&qf)[NKT]) {
     const IO* qp = static_cast<const IO*>(a.q) + (int64_t)e * a.bsq + h * D;
     if constexpr (kBufIO) {
@@ -1906,13 +1904,6 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 191) {
-    if (dense) hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, true>), grid, block, dyn, st, b);
-    else hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false, true>), grid, block, dyn, st, b);
-    return hipGetLastError();
-  }
-#endif
   if (dense)
     hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
   else

@@ -48,10 +48,9 @@ constexpr int group_occupancy() {
   return (D <= 40 && !(EDIT && STORE)) || (D <= 80 && !EDIT && !STORE) ? 2 : 1;
 }
 
-// LEGACY (experiments A/B only): the key mask by per-register compares, no mask column
-template <int D, int W, bool EDIT, bool STORE, bool LEGACY = false>
+template <int D, int W, bool EDIT, bool STORE>
 __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
-  constexpr bool kMaskCol = !LEGACY && (D + 15) / 16 * 16 > D;   // K column D carries the key mask
+  constexpr bool kMaskCol = (D + 15) / 16 * 16 > D;   // K column D carries the key mask
   constexpr int DK = (D + 15) / 16 * 16;
   constexpr int DV = (D + 31) / 32 * 32;
   constexpr int NKT = DK / 16;
@@ -314,7 +313,7 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
         // K made opaque per entry: hoisted out of the entry loop, the 16 per-register lane masks
         // were spilled to VGPR lanes and each restored by two v_readlane (plus a hazard s_nop)
         int Kl = K - kb * 32;
-        if constexpr (!LEGACY) asm volatile("" : "+s"(Kl));
+        asm volatile("" : "+s"(Kl));
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           if (acc_row(r, hh) >= Kl) sv[kb][r] = -INFINITY;
@@ -506,7 +505,7 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   }
 }
 
-template <int D, int W, bool LEGACY = false>
+template <int D, int W>
 hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   CrossArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
@@ -514,10 +513,10 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   const bool store = a.any_store != 0;
   const size_t dyn = store ? (size_t)W * 32 * a.K * sizeof(float) : 0;
   dim3 grid(b.n_qtiles * a.H * a.n_groups), block(64 * W);
-  if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true, LEGACY>), grid, block, dyn, st, b);
-  else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false, LEGACY>), grid, block, dyn, st, b);
-  else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true, LEGACY>), grid, block, dyn, st, b);
-  else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false, LEGACY>), grid, block, dyn, st, b);
+  if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
+  else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
+  else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
+  else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false>), grid, block, dyn, st, b);
   return hipGetLastError();
 }
 
@@ -547,7 +546,7 @@ bool cross_group_eligible(const CrossArgs& a, int d) {
 int run_cross_group(const CrossArgs& a, int d, hipStream_t st) {
   switch (d) {
 #ifdef P2P_EXPERIMENTS
-    case 40: return a.variant == 192 ? (int)launch_group<40, 4, true>(a, st) : (int)launch_group<40, 4>(a, st);
+    case 40: return (int)launch_group<40, 4>(a, st);
     case 80: return (int)launch_group<80, 4>(a, st);
     case 160: return (int)launch_group<160, 4>(a, st);
 #else

@@ -145,13 +145,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
   // every kernel argument the prologue reads is pinned here, so all of them arrive in ONE scalar
   // round trip (each a.field is a scalar load; hipcc otherwise spreads them over the prologue in a
   // chain of dependent waits); the entry's qk_src is the one dependent load after it
-  // (FORM bit 33554432, experiments A/B only: round 5's first prologue -- no pinning, a branch around
-  // every Q fragment load)
-  constexpr bool kLegacyQ = (FORM & 33554432) != 0;
-  if constexpr (!kLegacyQ)
-    asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v), "s"(a.o),
-                 "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv), "s"(a.bso),
-                 "s"(a.scale_log2));
+  asm volatile("" ::"s"(a.n_qtiles), "s"(a.H), "s"(a.P), "s"(a.K), "s"(a.q), "s"(a.k), "s"(a.v), "s"(a.o),
+               "s"(a.ldq), "s"(a.ldk), "s"(a.ldv), "s"(a.ldo), "s"(a.bsq), "s"(a.bsk), "s"(a.bsv), "s"(a.bso),
+               "s"(a.scale_log2));
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   auto stamp = [&](int idx) __attribute__((always_inline)) {
 #ifdef P2P_EXPERIMENTS
@@ -215,16 +211,9 @@ __global__ __launch_bounds__(64 * WAVES, WAVES >= 8 ? 2 : 1) void self40_kernel(
 #pragma unroll
       for (int t = 0; t < kNKT; ++t) {
         const int col = 16 * t + 8 * hh;
-        short8_t v;
-        if constexpr (kLegacyQ) {
-          const int p = pw + 32 * b + qi;
-          v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};
-          if (p < a.P && col < kD) v = *reinterpret_cast<const short8_t*>(qp + (int64_t)p * a.ldq + col);
-        } else {
-          v = __builtin_bit_cast(short8_t,
-                                 __builtin_amdgcn_raw_buffer_load_b128(rq, ((32 * b + qi) * (int)a.ldq + col) * 2, 0, 0));
-          if (col >= kD) v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};   // (d = 40: the padding columns 40..47)
-        }
+        short8_t v = __builtin_bit_cast(
+            short8_t, __builtin_amdgcn_raw_buffer_load_b128(rq, ((32 * b + qi) * (int)a.ldq + col) * 2, 0, 0));
+        if (col >= kD) v = short8_t{0, 0, 0, 0, 0, 0, 0, 0};   // (d = 40: the padding columns 40..47)
         if (prescale) {
           float mx = 0.f;
 #pragma unroll
@@ -698,7 +687,6 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
       case 110: return (int)launch<80, 4, 2, 128, false, 1>(a, st);      // round 4's default
       case 102: return (int)launch<80, 8, 1, 128, false, 1>(a, st);
       case 164: return (int)launch<80, 8, 1, 128, true, 1 | 128 | 256 | 512 | 16384 | 16>(a, st);  // default + stamps
-      case 190: return (int)launch<80, 8, 1, 128, true, 1 | 128 | 256 | 512 | 16384 | 33554432>(a, st);  // legacy Q prologue
 #endif
       // d = 80: 8 waves x ONE 32-row query block (two waves per SIMD), 128-key tiles, split staging
       // and the younger half's priority duty of the d = 40 kernel.  In the pipeline (bench.py,
@@ -712,7 +700,6 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
   switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
     case 163: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 16>(a, st);   // default with clock stamps
-    case 190: return (int)launch<40, 8, 2, 256, true, 17281 | 8388608 | 33554432>(a, st);   // legacy Q prologue
 #endif
     case 17281: return (int)launch<40, 8, 2, 256, true, 1 | 128 | 256 | 512 | 16384>(a, st);   // round-3 default
     // LEAN fragments, split staging (waves 0-3 K, 4-7 V), the younger half holding priority 1 on
