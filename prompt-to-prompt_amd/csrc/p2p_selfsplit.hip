@@ -321,6 +321,183 @@ __global__ __launch_bounds__(64 * W, 1) void self_ring_kernel(SelfArgs a) {
   }
 }
 
+// d = 160, 128 < K <= 256 (the 16x16 layers), all 256 CUs: one workgroup = 64 queries (two
+// 32-row blocks qb) of one (entry, head) x the two key HALVES kh: wave (qb, kh) streams the th =
+// ceil(ntiles / 2) 32-key tiles of its half through its half's 3-stage DMA ring, so each wave runs
+// half the serial tile chain of the 128-query ring kernel above on twice the workgroups; the
+// halves meet once at the end (O_1, m_1, l_1 through LDS into the kh = 0 wave).  Q arrives by DMA
+// too, in the same counted stream as the first tiles (the 128-query kernel drains its Q loads
+// with vmcnt(0) before the first DMA: one more round trip).  Per wave and tile exactly 11 DMA
+// instructions (the half's 11 K + 11 V split between its two waves), so the wait for tile s with
+// tile s + 1 in flight is vmcnt(11), and vmcnt(0) on the half's last tile.
+constexpr int kHalfStages = 3;
+constexpr int kHalfStageBytes = 22 * 1024;                   // K: 11 x 1 KiB (21-slot rows), V: 11
+constexpr int kHalfQBytes = 12 * 1024;                       // Q of one block: 12 x 1 KiB (21-slot rows)
+constexpr int kHalfLds = 2 * kHalfQBytes + 2 * kHalfStages * kHalfStageBytes;   // 156 KiB
+
+__global__ __launch_bounds__(256, 1) void self_halves_kernel(SelfArgs a) {
+  constexpr int D = 160, NKT = D / 16, NDT = D / 32, KCH = D / 8, KSL = KCH + 1;
+  constexpr float kThr = 8.0f;
+  __shared__ __attribute__((aligned(16))) char lds[kHalfLds];
+
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, qi = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qb = wave & 1, kh = wave >> 1;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % a.n_qtiles;
+  const int nh = logical / a.n_qtiles;
+  const int h = nh % a.H, n = nh / a.H;
+  const int src = a.qk_src[n];
+  const int K = a.K, P = a.P;
+  const float c = a.scale_log2;
+  const int ntiles = (K + 31) / 32;
+  const int th = (ntiles + 1) >> 1;          // tiles per half; half 1 starts at tile th < ntiles
+  const int t0 = kh * th;
+  const int q0 = qt * 64 + qb * 32;           // this wave's first query row
+  const uint16_t* const qp = static_cast<const uint16_t*>(a.q) + (int64_t)src * a.bsq + h * D;
+  const uint16_t* const kp = static_cast<const uint16_t*>(a.k) + (int64_t)src * a.bsk + h * D;
+  const uint16_t* const vp = static_cast<const uint16_t*>(a.v) + (int64_t)n * a.bsv + h * D;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  const uint32_t ring0 = lds0 + 2 * kHalfQBytes + kh * (kHalfStages * kHalfStageBytes);
+
+  // Q of block qb: 12 instructions of 21-slot rows (slot 20 and slots past row 31: padding), the
+  // block's two waves 6 each; rows past P read row P - 1 (never stored)
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int i = kh * 6 + j;
+    const int slot = i * 64 + lane;
+    int row = slot / KSL, ch = slot - row * KSL;
+    if (ch >= KCH || row >= 32) { row = 0; ch = 0; }
+    glds16(qp + (int64_t)min(q0 + row, P - 1) * a.ldq + ch * 8, __builtin_amdgcn_readfirstlane(lds0 + qb * kHalfQBytes + i * 1024));
+  }
+  // this wave's share of tile t0 + s of its half into stage s % 3: K instructions qb*6 .. (6 / 5),
+  // V instructions qb*5 .. (5 / 6; V's instruction 10 is padding)
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const uint32_t st = __builtin_amdgcn_readfirstlane(ring0 + (s % kHalfStages) * kHalfStageBytes);
+    const int kt = t0 + s;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const bool isk = qb == 0 ? j < 6 : j < 5;
+      const int i = qb == 0 ? (isk ? j : j - 6) : (isk ? 6 + j : j);   // instruction within K or V
+      const int slot = i * 64 + lane;
+      if (isk) {
+        int row = slot / KSL, ch = slot - row * KSL;
+        if (ch >= KCH || row >= 32) { row = 0; ch = 0; }
+        glds16(kp + (int64_t)min(kt * 32 + row, K - 1) * a.ldk + ch * 8, __builtin_amdgcn_readfirstlane(st + i * 1024));
+      } else {
+        int row = slot / KCH, ch = slot - row * KCH;
+        if (row >= 32) { row = 0; ch = 0; }
+        glds16(vp + (int64_t)min(kt * 32 + row, K - 1) * a.ldv + ch * 8,
+               __builtin_amdgcn_readfirstlane(st + 11 * 1024 + i * 1024));
+      }
+    }
+  };
+  issue(0);
+  if (th > 1) issue(1);
+
+  short8_t qf[NKT];
+  f32x16_t O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) O[dt] = f32x16_t{};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int s = 0; s < th; ++s) {
+    // this wave's DMAs of tile s (and, at s = 0, of Q) landed; tile s + 1 may still be in flight
+    if (s + 1 < th) __builtin_amdgcn_s_waitcnt(0x0F70 | 11);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();                           // ... and the other waves' shares
+    if (s == 0) {
+      const uint16_t* const Qs = reinterpret_cast<const uint16_t*>(lds + qb * kHalfQBytes);
+#pragma unroll
+      for (int t = 0; t < NKT; ++t) qf[t] = *reinterpret_cast<const short8_t*>(Qs + (qi * KSL + 2 * t + hh) * 8);
+    }
+    const char* const st = lds + 2 * kHalfQBytes + kh * (kHalfStages * kHalfStageBytes) + (s % kHalfStages) * kHalfStageBytes;
+    const uint16_t* const Kt = reinterpret_cast<const uint16_t*>(st);
+    const uint16_t* const Vt = reinterpret_cast<const uint16_t*>(st + 11 * 1024);
+    f32x16_t acc2[2] = {f32x16_t{}, f32x16_t{}};
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const short8_t kf = *reinterpret_cast<const short8_t*>(Kt + (qi * KSL + 2 * t + hh) * 8);
+      acc2[t & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, kf),
+                                                            __builtin_bit_cast(bf16x8_t, qf[t]), acc2[t & 1], 0, 0, 0);
+    }
+    const f32x16_t acc = acc2[0] + acc2[1];
+    // the stage read at s - 1 is free for tile s + 2 once every wave passed this barrier
+    if (s + 2 < th) issue(s + 2);
+    const int kt = t0 + s;
+    float sv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = acc[r];
+    if (kt * 32 + 32 > K) {                   // wave-uniform: only a tile reaching past K
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kt * 32 + acc_row(r, hh) >= K) sv[r] = -INFINITY;
+    }
+    float mx = sv[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sv[r]);
+    mx = fmaxf(mx, other_half(mx)) * c;        // -inf only for a tile wholly past K (never a half's first)
+    if (!__all(mx <= m_run + kThr)) {
+      const float mnew = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - mnew);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+      l_run *= alpha;
+      m_run = mnew;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sv[r] = fast_exp2(fmaf(sv[r], c, -m_run));
+      l_run += sv[r];
+    }
+    pv_block<D, NDT>(MmaBf16{}, O, Vt, 0, sv, lane);
+  }
+  __syncthreads();   // every wave is done with the rings (no DMA in flight: the last wait was vmcnt(0))
+
+  // ---- the halves meet: wave (qb, 1) hands (O, m, l) to wave (qb, 0) as 21 lane-major 16-byte
+  // chunks (conflict-free), then wave (qb, 0) writes the rows through LDS as 16-byte row chunks
+  f32x4_t* const part = reinterpret_cast<f32x4_t*>(lds) + qb * 21 * 64;
+  if (kh == 1) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        part[(dt * 4 + g) * 64 + lane] = f32x4_t{O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2], O[dt][4 * g + 3]};
+    part[20 * 64 + lane] = f32x4_t{m_run, l_run, 0.f, 0.f};
+  }
+  __syncthreads();
+  if (kh == 1) return;
+  const f32x4_t ml1 = part[20 * 64 + lane];
+  const float M = fmaxf(m_run, ml1[0]);
+  const float f0 = fast_exp2(m_run - M), f1 = fast_exp2(ml1[0] - M);
+  float l = l_run * f0 + ml1[1] * f1;
+  const float inv = 1.f / (l + other_half(l));
+  constexpr int OS = D + 8;
+  uint16_t* const orow = reinterpret_cast<uint16_t*>(lds + 2 * 21 * 1024) + qb * 32 * OS;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4_t o1 = part[(dt * 4 + g) * 64 + lane];
+      store4(orow + qi * OS + dt * 32 + 8 * g + 4 * hh, (O[dt][4 * g] * f0 + o1[0] * f1) * inv,
+             (O[dt][4 * g + 1] * f0 + o1[1] * f1) * inv, (O[dt][4 * g + 2] * f0 + o1[2] * f1) * inv,
+             (O[dt][4 * g + 3] * f0 + o1[3] * f1) * inv);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint16_t* const obase = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D;
+#pragma unroll
+  for (int c0 = 0; c0 < 32 * KCH; c0 += 64) {
+    const int cidx = c0 + lane;
+    const int row = cidx / KCH, ch = cidx - row * KCH;
+    const int pr = q0 + row;
+    if (pr < P)
+      *reinterpret_cast<short8_t*>(obase + (int64_t)pr * a.ldo + ch * 8) = *reinterpret_cast<const short8_t*>(orow + row * OS + ch * 8);
+  }
+}
+
 template <int D, int W, int KBW>
 hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
@@ -348,6 +525,17 @@ bool self_ring_eligible(const SelfArgs& a, int d) {
 
 int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
   (void)d;
+  bool halves = a.K <= 256;
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 200) halves = false;   // A/B: the 128-query ring kernel at every K
+#endif
+  if (halves) {
+    SelfArgs b = a;
+    b.n_qtiles = (a.P + 63) / 64;
+    dim3 grid(b.n_qtiles * a.H * a.N), block(256);
+    hipLaunchKernelGGL(self_halves_kernel, grid, block, 0, st, b);
+    return (int)hipGetLastError();
+  }
   return (int)launch_ring<4>(a, st);
 }
 

@@ -391,15 +391,17 @@ def test_cross_group_kernel_bf16(cuda, case):
         assert bsums[g][:, :, :2 * H].abs().max().item() == 0.0 and bsums[g][:, :, 3 * H:].abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("case", ["g3", "g4", "peaky32", "remap", "ragged", "k200", "k33", "k20"])
+@pytest.mark.parametrize("case", ["g3", "g4", "peaky32", "remap", "ragged", "k200", "k129", "k300", "k33", "k20"])
 def test_self_attention_key_split_d160(cuda, case):
     """d = 160 with bf16 inputs, O only (p2p_selfsplit.hip): K <= 128 takes the key-split kernel (the
     waves of a 32-query workgroup split the keys and combine (O_w, m_w, l_w) in LDS), larger K the
-    4-stage DMA ring kernel.  g4 / g3: the config-2 8x8 and 16x16 launches; ragged P / K, key-split
-    wave counts 1 and 2 (K = 20, 33, 77), K = 200 (a partial last ring tile), peaky rows (defer-max
-    rescales), a source remap."""
+    key-halves kernel up to K = 256 and the 4-stage DMA ring kernel past it.  g4 / g3: the config-2
+    8x8 and 16x16 launches; ragged P / K, key-split wave counts 1 and 2 (K = 20, 33, 77), K = 200 (a
+    partial last tile and a key half ending in a tile wholly past K), K = 129 (one key in the second
+    half's first tile), K = 300 (the ring kernel), peaky rows (defer-max rescales), a source remap."""
     N, P, K, H, d = {"g3": (8, 256, 256, 8, 160), "g4": (8, 64, 64, 8, 160), "ragged": (3, 100, 77, 2, 160),
-                     "k200": (2, 130, 200, 4, 160), "k33": (2, 70, 33, 2, 160),
+                     "k200": (2, 130, 200, 4, 160), "k129": (2, 97, 129, 2, 160),
+                     "k300": (2, 70, 300, 2, 160), "k33": (2, 70, 33, 2, 160),
                      "k20": (2, 45, 20, 2, 160)}.get(case, (4, 256, 256, 4, 160))
     q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=32.0 if case == "peaky32" else 1.0, seed=41)
     src = [0, 1, 0, 0] if case == "remap" else None
