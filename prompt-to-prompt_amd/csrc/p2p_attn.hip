@@ -1057,7 +1057,8 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #define P2P_CROSS_STAMP(i)
 #endif
 
-template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
+// XV: experiments-only compile-time variant (0 = production)
+template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE, int XV = 0>
 __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -1305,10 +1306,18 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
                                : nullptr;
   auto touch = [&]() __attribute__((always_inline)) {
     if (touch_when == 3) {
-      if (stored && a.store_accumulate) {
-        if (rmw_vec) rmw_load<kRmwF4>(sg, srows * K, lane, rmwbuf);
-        if (blend_on && qi < srows) bsum_old = *bdst;
-      }
+      // issued unconditionally (zero-size buffer resources when nothing is kept: no traffic), so
+      // every path issues the same number of loads here -- a branch-skipped load makes hipcc's waits
+      // for the prologue's loads count on the path without it (the dense prologue below)
+      const bool acc = stored && a.store_accumulate;
+      rmw_load<kRmwF4>(sg, (acc && rmw_vec) ? srows * K : 0, lane, rmwbuf);
+      // the lane's LocalBlend word-sum entry: (b * 2 + hh)'s plane, query p0w + qi (lanes past the
+      // rows read a neighbour or zero, and keep 0)
+      const bool bl = acc && blend_on;
+      const float* const bb = bl ? a.grp_bsum[gi] + ((int64_t)(b * 2) * a.grp_blh[gi] + a.grp_bcol[gi] + h) * a.P + p0w : nullptr;
+      const __amdgpu_buffer_rsrc_t rb = make_rsrc(bb, bl ? ((int64_t)a.grp_blh[gi] * a.P + srows) * 4 : 0);
+      const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, (hh * a.grp_blh[gi] * a.P + qi) * 4, 0, 0));
+      bsum_old = qi < srows ? v : 0.f;
     } else if (stored && a.store_accumulate) {
       const int rows = min(32, a.P - p0w);
       const float* g = a.store + ((int64_t)(slot + h) * a.P + p0w) * (int64_t)K;
@@ -1483,16 +1492,17 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     const uint16_t* mg = static_cast<const uint16_t*>(a.grp_dense[gi]) +
                          (int64_t)(b - 1) * P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE;
     EV* const Ms = reinterpret_cast<EV*>(cross_dyn);  // [96 source words][96 target words]
-    // every global load of the prologue first (mapper tile chunks, coefficients, the source's Q
-    // and K), then the LDS writes: one memory round trip instead of a chain of them
+    // every global load of the prologue is issued at once (one memory round trip), in the order
+    // of use: the coefficients and the source's K and Q (P0), then the mapper tile (R) and this
+    // entry's own rows.  Each is waited for only where it is used, so the in-order counter lets
+    // P0 start once the source's bytes have landed while the tile and the own V land behind it:
+    // the launch-wide prologue burst, not the latency, sets the first round trip.
+    // d = 160 only: at d <= 80 (two workgroups per CU, 256 VGPRs) the tile and the own V held in
+    // registers across P0 spill 56 VGPRs
+    // (XV 201, experiments A/B: the tile and the own V staged before the first barrier)
+    constexpr bool late = D > 80 && XV != 201;
     constexpr int kMCh = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE / 8;   // 16-byte chunks of the tile
     constexpr int kMPer = (kMCh + NT - 1) / NT;
-    short8_t mreg[kMPer];
-#pragma unroll
-    for (int j = 0; j < kMPer; ++j) {
-      const int i = tid + j * NT;
-      if (i < kMCh) mreg[j] = reinterpret_cast<const short8_t*>(mg)[i];
-    }
     const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
                                                      (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES);
     const float* al = a.grp_alpha[gi] + (b - 1) * K;
@@ -1507,20 +1517,38 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     Chunk8<IO> kc0[NCH], vc0[NCH];
     load_kv(first, kc0, vc0, false);
     load_q(first, qf);
-    own_early = !r_only;
-    if (own_early) {
-      load_kv(n, kc1, vc1, true);
-      load_q(n, qf1);
-    } else if (r_only) {
-      load_kv(n, kc1, vc1, true, false);   // own V only
+    // (the scheduler would otherwise issue the Q loads last, and every wait for Q would then wait
+    // for the tile and the own rows as well)
+    __builtin_amdgcn_sched_barrier(0);
+    // the tile by range-checked buffer loads (chunks past it read as zeros), the own V on both
+    // paths, and only then the path-dependent own K and Q: hipcc's wait for a load counts the
+    // loads issued after it on the path that issued the FEWEST, so a branch-skipped load between
+    // Q and its use would make the R_ONLY path wait for the tile and the own V before P0
+    short8_t mreg[kMPer];
+    {
+      const __amdgpu_buffer_rsrc_t rm = make_rsrc(mg, (int64_t)kMCh * 16);
+#pragma unroll
+      for (int j = 0; j < kMPer; ++j)
+        mreg[j] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rm, (tid + j * NT) * 16, 0, 0));
     }
+    __builtin_amdgcn_sched_barrier(0);
+    own_early = !r_only;
+    load_kv(n, kc1, vc1, true, false);   // own V
+    __builtin_amdgcn_sched_barrier(0);
+    if (own_early) {
+      load_kv(n, kc1, vc1, false, true);   // own K
+      load_q(n, qf1);
+    }
+    auto store_tile = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < kMPer; ++j) {
+        const int i = tid + j * NT;
+        if (i < kMCh) reinterpret_cast<short8_t*>(Ms)[i] = mreg[j];
+      }
+    };
     finish_prologue();
     P2P_CROSS_STAMP(19)
-#pragma unroll
-    for (int j = 0; j < kMPer; ++j) {
-      const int i = tid + j * NT;
-      if (i < kMCh) reinterpret_cast<short8_t*>(Ms)[i] = mreg[j];
-    }
+    if (!late) store_tile();
     P2P_CROSS_STAMP(20)
     {  // per-column coefficients next to the tile, read back after the barriers:
       // P' = alpha*post*(c_rep*P_b + R) + (1-alpha)*P_b = P_b*A + R*B
@@ -1533,9 +1561,9 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     }
     P2P_CROSS_STAMP(21)
     store_kv(kc0, vc0, false);
-    // R_ONLY: the own V goes to its LDS image now (the P0 / R phase reads only K and the mapper),
-    // so no second staging phase follows
-    if (r_only) store_kv(kc1, vc1, true, false);
+    // R_ONLY: the own V goes to its LDS image in this phase (the P0 / R phase reads only K and the
+    // mapper), so no second staging phase follows
+    if (r_only && !late) store_kv(kc1, vc1, true, false);
     P2P_CROSS_STAMP(22)
     __syncthreads();
     if (touch_when == 1 || touch_when == 3) touch();
@@ -1556,6 +1584,10 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     if (dense_flags & 2) {
     float p0[KB][16];
     probs(qf, p0);
+    if (late) {
+      store_tile();      // (workgroup-uniform branch: every wave reads the same coefficients)
+      __syncthreads();
+    }
     P2P_CROSS_STAMP(9)
     // R = M^T P0 on the f16 MFMA: the mapper weights (1, 1/2, 1/4, ...) are exact in f16 and P0 in
     // [0, 1] rounds to 11 significant bits (|dR| <= 2^-12 R, inside the 2e-3 bar); every mapper
@@ -1585,6 +1617,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     } else if (!r_only || (dense_flags & 1)) {
       load_q(n, qf);
     }
+    if (r_only && late) store_kv(kc1, vc1, true, false);   // (V is read only after the barrier below)
     __syncthreads();  // every wave is done with the source K tile and the mapper tile
     P2P_CROSS_STAMP(10)
    }
@@ -1904,6 +1937,12 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
+#ifdef P2P_EXPERIMENTS
+  if (dense && a.variant == 201 && D > 80) {
+    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 201>), grid, block, dyn, st, b);
+    return hipGetLastError();
+  }
+#endif
   if (dense)
     hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
   else

@@ -4,6 +4,9 @@
 # production kernels), A B A B, each a rocprofv3 --kernel-trace --stats run of bench.py.
 # Push with tools/gpu_ab.sh (EXTRA_CXXFLAGS in the env so its make keeps the flags):
 #   EXTRA_CXXFLAGS=-fno-slp-vectorize tools/gpu_ab.sh --timeout 900 -- 'bash tools/gpu_flag_ab.sh r05slp'
+# With VA / VB set, both sides run the experiments library, A under P2P_SELF_VARIANT=$VA and B
+# under $VB (a variant A/B without the production-vs-experiments build difference):
+#   tools/gpu_ab.sh --timeout 900 -- 'VA=0 VB=201 bash tools/gpu_flag_ab.sh r05v201'
 set -u
 export TMPDIR=/tmp
 tag=${1:-flagab}
@@ -14,7 +17,10 @@ i=0
 for lib in A B A B; do
   i=$((i + 1))
   d="$out/prof_${lib}$i"
-  if [ $lib = B ]; then export P2P_EXPERIMENTS_LIB=1; else unset P2P_EXPERIMENTS_LIB; fi
+  if [ -n "${VA:-}" ]; then
+    export P2P_EXPERIMENTS_LIB=1
+    if [ $lib = A ]; then export P2P_SELF_VARIANT=$VA; else export P2P_SELF_VARIANT=$VB; fi
+  elif [ $lib = B ]; then export P2P_EXPERIMENTS_LIB=1; else unset P2P_EXPERIMENTS_LIB; fi
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 -u bench.py $args > "$out/run_${lib}$i.log" 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "FAILED rc=$rc ($lib$i)"; tail -30 "$out/run_${lib}$i.log"; exit $rc; fi
