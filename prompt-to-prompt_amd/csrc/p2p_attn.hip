@@ -1136,6 +1136,60 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   const float c = a.scale_log2;
   const int P0S = a.slab_stride;
   float* const slab = reinterpret_cast<float*>(cross_dyn) + wave * 32 * P0S;
+  // O out.  The accumulator puts the query on the lane, so a direct store writes 32 rows x 8 bytes
+  // per instruction.  bf16 outputs with 16-byte rows instead go through LDS (the self kernels'
+  // epilogue): after a workgroup barrier (every wave is done with K / V) each wave writes its 32
+  // rows into the dead K / V image and stores them back as whole 16-byte row chunks, consecutive
+  // lanes along a row -- half the store instructions, whole lines.  (XV 202, experiments A/B: the
+  // direct store.)
+  // Same-box rocprof (profiles/r05/ostore_ab/): d = 80 edit steps 16.43 -> 14.90 us, d = 160 17.44 ->
+  // 16.56; the 8x8 layers (P = 64: half of every 128-query workgroup's rows past P) ran 2 % slower
+  // and keep the direct store
+  const bool o16 = std::is_same<IO, uint16_t>::value && XV != 202 && a.P >= 256 && (a.ldo & 7) == 0 &&
+                   (a.bso & 7) == 0 && ((uintptr_t)a.o & 15) == 0;
+  auto store_o = [&](const f32x16_t (&O)[NDT], float inv) __attribute__((always_inline)) {
+    if constexpr (std::is_same<IO, uint16_t>::value) {
+      if (o16) {
+        constexpr int OS = D + 8;   // 16-byte aligned rows on distinct banks
+        static_assert(WAVES * 32 * OS * 2 <= KBYTES + VBYTES, "the output rows fit the K / V image");
+        __syncthreads();
+        uint16_t* const orow = reinterpret_cast<uint16_t*>(smem) + wave * 32 * OS;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int dd = dt * 32 + 8 * g + 4 * hh;
+            if (dd < D)
+              store4(orow + qi * OS + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
+                     O[dt][4 * g + 3] * inv);
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint16_t* const ob = static_cast<uint16_t*>(a.o) + (int64_t)n * a.bso + h * D;
+#pragma unroll
+        for (int c0 = 0; c0 < 32 * CPR; c0 += 64) {
+          const int cidx = c0 + lane;
+          const int row = cidx / CPR, ch = cidx - row * CPR;
+          if (((32 * CPR) % 64 == 0 || cidx < 32 * CPR) && p0w + row < a.P)
+            *reinterpret_cast<short8_t*>(ob + (int64_t)(p0w + row) * a.ldo + ch * 8) =
+                *reinterpret_cast<const short8_t*>(orow + row * OS + ch * 8);
+        }
+        return;
+      }
+    }
+    if (prow) {
+      IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = dt * 32 + 8 * g + 4 * hh;
+          if (dd < D)
+            store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv, O[dt][4 * g + 3] * inv);
+        }
+    }
+  };
 
   // ---- plain entries (no edit program, maps not kept): the lean path.  Every global load is
   // issued first (Q fragments, this thread's K and V chunks) and the padding is written while they
@@ -1237,18 +1291,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
       for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
       P2P_CROSS_STAMP(4)
       const float inv = 1.f / __shfl(O[kLdt][kLr], (lane & 31) + 32 * kLh);
-      if (prow) {
-        IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D + (int64_t)p * a.ldo;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int dd = dt * 32 + 8 * g + 4 * hh;
-            if (dd < D)
-              store4(op + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
-                     O[dt][4 * g + 3] * inv);
-          }
-      }
+      store_o(O, inv);
       P2P_CROSS_STAMP(5)
       return;
     }
@@ -1825,18 +1868,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) pv_block<VS, NDT>(MP{}, O, Vs, kb * 32, sv[kb], lane);
   P2P_CROSS_STAMP(15)
-  if (prow) {
-    IO* const op = static_cast<IO*>(a.o) + (int64_t)n * a.bso + h * D;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int dd = dt * 32 + 8 * g + 4 * hh;
-        if (dd < D)
-          store4(op + (int64_t)p * a.ldo + dd, O[dt][4 * g], O[dt][4 * g + 1], O[dt][4 * g + 2],
-                 O[dt][4 * g + 3]);
-      }
-  }
+  store_o(O, 1.f);
 }
 
 // ====================================================================== launchers
@@ -1940,6 +1972,11 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
 #ifdef P2P_EXPERIMENTS
   if (dense && a.variant == 201 && D > 80) {
     hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 201>), grid, block, dyn, st, b);
+    return hipGetLastError();
+  }
+  if (a.variant == 202) {
+    if (dense) hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 202>), grid, block, dyn, st, b);
+    else hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false, 202>), grid, block, dyn, st, b);
     return hipGetLastError();
   }
 #endif
