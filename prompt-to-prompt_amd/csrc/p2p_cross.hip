@@ -48,7 +48,8 @@ constexpr int group_occupancy() {
   return (D <= 40 && !(EDIT && STORE)) || (D <= 80 && !EDIT && !STORE) ? 2 : 1;
 }
 
-template <int D, int W, bool EDIT, bool STORE>
+// XV: experiments-only compile-time variant (0 = production)
+template <int D, int W, bool EDIT, bool STORE, int XV = 0>
 __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
   constexpr bool kMaskCol = (D + 15) / 16 * 16 > D;   // K column D carries the key mask
   constexpr int DK = (D + 15) / 16 * 16;
@@ -72,6 +73,14 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   __shared__ __attribute__((aligned(16))) float coef[EDIT ? 2 * KR : 4];      // A | B of the entry
   __shared__ __attribute__((aligned(16))) float btab[STORE ? 2 * KR : 4];     // blend alpha | substruct
   extern __shared__ __attribute__((aligned(16))) char cross_dyn[];           // STORE: W x [32][K] f32
+  // each wave's output rows on their way out (wave-private: no workgroup barrier)
+  // Plain groups only.  Same-box rocprof (profiles/r05/ostore_ab/group/): plain steps 17.23 -> 15.77
+  // us, but edit steps 19.29 -> 19.53 (the 12 KiB of rows beside the mapper tile), so the edit
+  // instantiations keep the direct row-per-lane store, as does plain + store (at two workgroups
+  // per CU the extra addressing spilled 6 VGPRs).  (XV 202, experiments A/B: the direct store.)
+  constexpr bool kLdsOut = XV != 202 && !EDIT && !STORE;
+  constexpr int OS = D + 8;             // 16-byte aligned rows on distinct banks
+  __shared__ __attribute__((aligned(16))) uint16_t Os[kLdsOut ? W * 32 * OS : 8];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -474,7 +483,38 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     constexpr int kLh = (kLrr >> 2) & 1;
     constexpr int kLr = (kLrr & 3) + 4 * (kLrr >> 3);
     const float inv = lean ? 1.f / __shfl(O[kOnesCol ? D / 32 : 0][kLr], (lane & 31) + 32 * kLh) : 1.f;
-    if (prow) {
+    // O out: the accumulator puts the query on the lane, so a direct store writes 32 rows x 8 bytes
+    // per instruction; the wave's 32 rows go through its LDS rows instead and leave as whole
+    // 16-byte row chunks, consecutive lanes along a row (the per-entry kernel's epilogue)
+    const bool o16 = kLdsOut && (a.ldo & 7) == 0 && (a.bso & 7) == 0 && ((uintptr_t)a.o & 15) == 0;
+    if (o16) {
+      uint16_t* const orow = Os + wave * 32 * OS;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dd = dt * 32 + 8 * g + 4 * hh;
+          if (dd < D)
+            store4(orow + qi * OS + dd, O[dt][4 * g] * inv, O[dt][4 * g + 1] * inv, O[dt][4 * g + 2] * inv,
+                   O[dt][4 * g + 3] * inv);
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint16_t* const ob = static_cast<uint16_t*>(a.o) + (int64_t)e * a.bso + h * D;
+#pragma unroll
+      for (int c0 = 0; c0 < 32 * CPR; c0 += 64) {
+        const int cidx = c0 + lane;
+        const int row = cidx / CPR, ch = cidx - row * CPR;
+        if (((32 * CPR) % 64 == 0 || cidx < 32 * CPR) && p0w + row < P)
+          *reinterpret_cast<short8_t*>(ob + (int64_t)(p0w + row) * a.ldo + ch * 8) =
+              *reinterpret_cast<const short8_t*>(orow + row * OS + ch * 8);
+      }
+      // the next entry rewrites these rows: every lane's reads first
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (prow) {
       uint16_t* const op = static_cast<uint16_t*>(a.o) + (int64_t)e * a.bso + h * D + (int64_t)p * a.ldo;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
@@ -513,6 +553,15 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   const bool store = a.any_store != 0;
   const size_t dyn = store ? (size_t)W * 32 * a.K * sizeof(float) : 0;
   dim3 grid(b.n_qtiles * a.H * a.n_groups), block(64 * W);
+#ifdef P2P_EXPERIMENTS
+  if (a.variant == 202) {
+    if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true, 202>), grid, block, dyn, st, b);
+    else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false, 202>), grid, block, dyn, st, b);
+    else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true, 202>), grid, block, dyn, st, b);
+    else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false, 202>), grid, block, dyn, st, b);
+    return hipGetLastError();
+  }
+#endif
   if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
   else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
   else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
