@@ -77,9 +77,15 @@ class FenceFreeEvent:
             raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
 
     def __del__(self):
-        if self.ev.value and self._hip is not None:
-            self._hip.hipEventDestroy(self.ev)
-            self.ev = self._ctypes.c_void_p()
+        # may run at interpreter shutdown (after the HIP runtime is gone) or after a failed __init__
+        ev, hip = getattr(self, "ev", None), FenceFreeEvent._hip
+        if ev is None or not ev.value or hip is None:
+            return
+        try:
+            hip.hipEventDestroy(ev)
+        except Exception:
+            pass
+        self.ev = None
 
     def record(self):
         rc = self._lib().hipEventRecord(self.ev, ctypes_stream())
@@ -97,6 +103,48 @@ class FenceFreeEvent:
 def ctypes_stream():
     import ctypes
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+NOMINAL_SCLK_MHZ = 2400.0       # the clock the dense peak assumes: 256 CU x 4 SIMD x 1024 FLOP/cycle x 2.4 GHz
+
+
+class ClockProbe:
+    """The shader clock the chip holds during the timed run (p2p_clock_probe, include/p2p_hip.h):
+    8 one-wave workgroups (one per XCD) each count shader cycles against the constant 100 MHz
+    counter over `ticks` (10 us).  Sampled at the start and the end of the timed region and right
+    after every `every`-th dominant-kernel launch (after its end event, so it sits in no attention
+    launch's timing window): DVFS moves the clock on a millisecond scale, so a probe queued right
+    behind the G1/G7 kernel reads the clock the chip was holding for it.  Each sample = the median
+    over the 8 workgroups."""
+
+    def __init__(self, device, max_samples=512, every=25, ticks=1000):
+        from p2p_amd import _hip
+        self._hip = _hip
+        self.buf = torch.zeros(max_samples, 8, 2, dtype=torch.int64, device=device)
+        self.tags, self.every, self.ticks, self.n_dominant = [], every, ticks, 0
+
+    def sample(self, tag):
+        if len(self.tags) < self.buf.shape[0]:
+            self._hip.clock_probe(self.buf[len(self.tags)], self.ticks)
+            self.tags.append(tag)
+
+    def after_dominant(self):
+        self.n_dominant += 1
+        if self.n_dominant % self.every == 0:
+            self.sample("pipeline")
+
+    def summary(self):
+        torch.cuda.synchronize()
+        n = len(self.tags)
+        if not n:
+            return None
+        b = self.buf[:n].double().cpu()
+        mhz = (b[..., 0] / b[..., 1].clamp(min=1) * 100.0).median(dim=1).values.tolist()
+        pipe = sorted(m for m, t in zip(mhz, self.tags) if t == "pipeline")
+        edge = {t: round(m, 1) for m, t in zip(mhz, self.tags) if t != "pipeline"}
+        return {"sclk_mhz": (pipe[len(pipe) // 2] if pipe else sorted(mhz)[n // 2]),
+                "pipeline_samples": len(pipe), "pipeline_min_mhz": pipe[0] if pipe else None,
+                "pipeline_max_mhz": pipe[-1] if pipe else None, **{f"{k}_mhz": v for k, v in edge.items()}}
 
 
 class LaunchTimer:
@@ -120,6 +168,7 @@ class LaunchTimer:
         self.batch = 0
         self.batch_marks = []    # one event at the end of each timed batch
         self.cross_group_kernel = {}   # geometry name -> True when the group cross kernel ran
+        self.clock = None              # a ClockProbe sampled behind the dominant kernel
 
     @staticmethod
     def _bytes(kind, t, info):
@@ -159,6 +208,8 @@ class LaunchTimer:
             for name, work in names:
                 self.rec.setdefault(name, []).append((start, ev, work, self.batch))
             self._pending = None
+            if self.clock is not None and any(n == "dominant" for n, _ in names):
+                self.clock.after_dominant()
 
     def before_aux(self, name, nbytes):
         """The LocalBlend mask and latent-step launches (HBM-type helpers), with their bytes."""
@@ -225,7 +276,10 @@ class LaunchTimer:
                 "bound": "hbm", "achieved": kind_bytes["cross"] / (kind_ms["cross"] * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": kind_bytes["cross"] / (kind_ms["cross"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                "ms_per_unet_call": kind_ms["cross"] / unet_calls if unet_calls else None},
+                "ms_per_unet_call": kind_ms["cross"] / unet_calls if unet_calls else None,
+                "bytes_model": "algorithmic lower bound: q + k + v read once, o written once, kept maps read + "
+                               "written; the edits' re-reads of the source rows and their mapper tiles are "
+                               "not counted (PMC FETCH_SIZE / WRITE_SIZE per launch: profiles/r05/pmc/table.md)"},
         }
         return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                 "by_kind": by_kind,
@@ -275,6 +329,20 @@ class LaunchTimer:
                         "bytes_rule": rules.get(name, "q + o + k + v (io dtype) + kept maps f32 x2 (read + write, "
                                                       "steps >= 1)")})
         return out
+
+
+def _clock_fields(clk, frac):
+    """roofline.sclk_mhz (the measured shader clock) and frac_at_measured_clock (the same achieved
+    rate against the peak scaled to that clock): what separates box-to-box clock spread from a
+    kernel change."""
+    if not clk:
+        return {"sclk_mhz": None, "frac_at_measured_clock": None}
+    return {"sclk_mhz": clk["sclk_mhz"], "nominal_sclk_mhz": NOMINAL_SCLK_MHZ,
+            "frac_at_measured_clock": frac * NOMINAL_SCLK_MHZ / clk["sclk_mhz"] if frac else None,
+            "clock_probe": {**clk, "rule": "p2p_clock_probe: 8 one-wave workgroups count shader cycles over 10 us "
+                                           "of the 100 MHz counter; sampled after every 25th G1/G7 launch and at "
+                                           "the start / end of the timed region; sclk = median of the in-pipeline "
+                                           "samples"}}
 
 
 def pmc_traffic():
@@ -414,9 +482,12 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    clock = ClockProbe(dev)
+    timer.clock = clock
     timer.enabled = True
     t0 = time.perf_counter()
 
+    clock.sample("start")
     timer.end_batch()     # (batch 0's start mark)
 
     def progress(i, n):   # a progress line per batch (stderr; host-side only) + the batch's end event
@@ -429,6 +500,7 @@ def main():
     # all-gather of the final latents and the reduced maps (the only inter-GPU traffic)
     lat_all, maps_all = sweep.run_batched_sweep(all_seeds, batch, batch.out_shapes, rank, world, G,
                                                 device=dev, on_batch=progress)
+    clock.sample("end")
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -464,6 +536,7 @@ def main():
                               f"256-key tiles, software-pipelined 32x32 blocks)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops,
+                    **_clock_fields(clock.summary(), (achieved / peak) if achieved else None),
                     "timing": ("HIP events around each launch on its stream, created with hipEventDisableSystemFence"
                                if args.launch_events == "fence-free" else "torch.cuda.Event around each launch")}
         cpu = None

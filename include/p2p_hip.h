@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 14
+#define P2P_ABI_VERSION 15
 #define P2P_MAX_BATCH 64  /* entries per launch (U-Net batch: 2 x prompts x groups)   */
 #define P2P_MAX_GROUPS 32 /* prompt groups per cross-attention launch                 */
 #define P2P_MAX_KEYS_CROSS 96
@@ -244,6 +244,14 @@ int p2p_latent_step(const p2p_latent_step_args* a, p2p_stream_t stream);
  * src * (1.0f / divisor) -- what torch does for `cuda_tensor / python_scalar` on the
  * reference's cuda:0 device. */
 int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_stream_t stream);
+
+/* Measurement only (ABI 15; bench.py's roofline clock, not part of the reference's interface):
+ * n_workgroups one-wave workgroups each read the shader-cycle counter and the constant 100 MHz
+ * counter, spin until `ticks` (1..1e6) of the 100 MHz counter have passed, and read both again:
+ * out[2 w] = shader cycles, out[2 w + 1] = 100 MHz ticks of workgroup w, so the shader clock is
+ * out[2 w] / out[2 w + 1] x 100 MHz.  Consecutive workgroups run on different XCDs.  out: device
+ * memory, 2 x n_workgroups (1..1024) u64. */
+int p2p_clock_probe(uint64_t* out, int32_t n_workgroups, int32_t ticks, p2p_stream_t stream);
 
 /* Build/runtime information.  p2p_source_hash: content hash of the HIP sources the library
  * was built from (p2p_amd/_srchash.py), so a host can refuse a stale prebuilt binary. */

@@ -266,6 +266,27 @@ __global__ void store_scale_kernel(const float* __restrict__ src, float* __restr
     dst[i] = src[i] * inv;
 }
 
+// ---------------------------------------------------------------- shader-clock probe
+// Measurement only (bench.py's roofline clock): one wave per workgroup.  Each wave reads the
+// shader-cycle counter (s_memtime: one tick per shader clock) and the constant 100 MHz counter
+// (s_memrealtime), spins on the 100 MHz counter until `ticks` of it have passed, and reads both
+// again -- clock = d(cycles) / d(ticks) x 100 MHz.  Both pairs are read in the same order, so the
+// two windows are offset by the same read latency.  Consecutive workgroups land on different XCDs
+// (round-robin dispatch), so n workgroups >= 8 sample every XCD.  Lanes 0 / 1 store (vector
+// stores): out[2 wg] = cycles, out[2 wg + 1] = ticks.
+__global__ void clock_probe_kernel(unsigned long long* __restrict__ out, unsigned ticks) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long r1 = r0;
+  while (r1 - r0 < ticks) {
+    __builtin_amdgcn_s_sleep(2);
+    r1 = __builtin_amdgcn_s_memrealtime();
+  }
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x < 2) out[2 * blockIdx.x + threadIdx.x] = threadIdx.x == 0 ? c1 - c0 : r1 - r0;
+}
+
 // ---------------------------------------------------------------- fused latent update
 // One denoising step's latent update (ptp_utils.py:72-75): classifier-free guidance
 // (:73), the DDIM step (diffusers DDIMScheduler.step with eta = 0, restated by the reference as
@@ -478,6 +499,11 @@ int run_localblend(const p2p_blend_args& a, hipStream_t st) {
   dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map, (a.map_res * a.map_res + kWsPix - 1) / kWsPix);
   if (!a.word_sums_ready) hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
   hipLaunchKernelGGL(blend_finalize_kernel, dim3(a.n_prompts), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+int run_clock_probe(unsigned long long* out, int n_wg, int ticks, hipStream_t st) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3((unsigned)n_wg), dim3(64), 0, st, out, (unsigned)ticks);
   return (int)hipGetLastError();
 }
 

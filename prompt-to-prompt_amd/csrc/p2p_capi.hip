@@ -296,4 +296,9 @@ int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_
   return run_store_scale(src, dst, divisor, n, (hipStream_t)stream);
 }
 
+int p2p_clock_probe(uint64_t* out, int32_t n_workgroups, int32_t ticks, p2p_stream_t stream) {
+  if (!out || n_workgroups < 1 || n_workgroups > 1024 || ticks < 1 || ticks > 1000000) return P2P_E_ARG;
+  return run_clock_probe(reinterpret_cast<unsigned long long*>(out), n_workgroups, ticks, (hipStream_t)stream);
+}
+
 }  // extern "C"

@@ -111,5 +111,6 @@ struct BwdArgs {
 int run_attn_bwd(const BwdArgs& a, int io_dtype, int d, hipStream_t st);
 int bwd_kv_split(int N, int H, int P, int K, int d);   // launcher's query split (workspace sizing)
 int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipStream_t st);
+int run_clock_probe(unsigned long long* out, int n_wg, int ticks, hipStream_t st);
 
 }  // namespace p2p

@@ -32,7 +32,7 @@ MAX_GROUPS = 32
 MAX_KEYS_CROSS = 96
 PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
-ABI_VERSION = 14
+ABI_VERSION = 15
 GROUP_F_R_ONLY = 2      # p2p_group.flags: every edit's blend coefficient A is 0 this call (P' = R)
 
 
@@ -113,8 +113,10 @@ def lib():
         L.p2p_attn_bwd.argtypes = [ctypes.POINTER(AttnTensors), vp, vp, vp, vp, vp, vp, i32, vp, i64, vp]
         L.p2p_attn_bwd_workspace.argtypes = [ctypes.POINTER(AttnTensors)]
         L.p2p_attn_bwd_workspace.restype = ctypes.c_int64
+        L.p2p_clock_probe.argtypes = [vp, i32, i32, vp]
         for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
-                   "p2p_localblend", "p2p_store_scale", "p2p_latent_step", "p2p_attn_fwd_lse", "p2p_attn_bwd"):
+                   "p2p_localblend", "p2p_store_scale", "p2p_latent_step", "p2p_attn_fwd_lse", "p2p_attn_bwd",
+                   "p2p_clock_probe"):
             getattr(L, fn).restype = ctypes.c_int
         if L.p2p_abi_version() != ABI_VERSION:
             raise HipError(f"libp2p_hip.so ABI {L.p2p_abi_version()} != {ABI_VERSION}")
@@ -139,7 +141,18 @@ def check_source_hash() -> str:
 
 EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_source_hash", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
                     "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step",
-                    "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace")
+                    "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace", "p2p_clock_probe")
+
+
+def clock_probe(out: torch.Tensor, ticks: int = 1000):
+    """Measurement only (bench.py): one p2p_clock_probe launch on the current stream, one one-wave
+    workgroup per row of ``out`` (int64 [n, 2] on the GPU: shader cycles, 100 MHz ticks); the
+    shader clock of row w is out[w, 0] / out[w, 1] x 100 MHz, read after a synchronise."""
+    _require_cuda(out)
+    if out.dtype != torch.int64 or out.dim() != 2 or out.shape[1] != 2 or not out.is_contiguous():
+        raise HipError("clock_probe needs a contiguous int64 [n, 2] tensor")
+    _check(lib().p2p_clock_probe(out.data_ptr(), out.shape[0], int(ticks), _stream(out.device)), "p2p_clock_probe")
+    return out
 
 
 def _check(rc: int, what: str):

@@ -536,9 +536,12 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         Decided once per step (the alpha table is copied to the host once)."""
         prog = self._device_program(device)
         alpha = self.cross_replace_alpha
-        held = self._alpha_host   # (the tensor itself, its version, host copy): identity, not id()
-        if held is None or held[0] is not alpha or held[1] != alpha._version:
-            held = self._alpha_host = (alpha, alpha._version, alpha.detach().to("cpu", torch.float64).numpy())
+        # (the tensor itself, its version, host copy): identity, not id().  A tensor made under
+        # torch.inference_mode() has no version counter: its storage address stands in for it
+        version = ("ptr", alpha.data_ptr()) if alpha.is_inference() else alpha._version
+        held = self._alpha_host
+        if held is None or held[0] is not alpha or held[1] != version:
+            held = self._alpha_host = (alpha, version, alpha.detach().to("cpu", torch.float64).numpy())
             self._step_cache = {}
         key = (self.cur_step, K)
         hit = self._step_cache.get(key)

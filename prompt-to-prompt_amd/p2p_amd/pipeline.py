@@ -129,7 +129,7 @@ def run_edit_groups(model: SyntheticStableDiffusion, prompt_groups: Sequence[Seq
     ptp_utils.register_attention_control(model, controller)
     text = ptp_utils._encode(model, prompts, model.text_encoder)
     uncond = ptp_utils._encode(model, [""] * len(prompts), model.text_encoder)
-    context = torch.cat([uncond, text])
+    context = ptp_utils.unet_context(model, torch.cat([uncond, text]))
     latents = torch.cat([x.reshape(1, 4, 64, 64).expand(B, 4, 64, 64) for x in x_Ts]).to(model.device)
     model.scheduler.set_timesteps(num_steps)
     for t in model.scheduler.timesteps:

@@ -107,6 +107,19 @@ def _encode(model, prompts, encoder):
     return encoder(ids.to(model.device))[0]
 
 
+def unet_context(model, context):
+    """The context in the U-Net's own dtype, cast once before the sampling loop: a U-Net that
+    casts ``encoder_hidden_states`` itself then gets back this same tensor at every step (a cast
+    to its own dtype is a no-op), which keeps the cross-attention K / V cache of _cross_kv valid
+    across steps."""
+    dtype = getattr(model.unet, "dtype", None)
+    if not isinstance(dtype, torch.dtype):
+        return context
+    if isinstance(context, (list, tuple)):
+        return type(context)(c.to(dtype) for c in context)
+    return context.to(dtype)
+
+
 @torch.no_grad()
 def text2image_ldm(model, prompt: List[str], controller, num_inference_steps: int = 50,
                    guidance_scale: Optional[float] = 7., generator: Optional[torch.Generator] = None,
@@ -118,7 +131,7 @@ def text2image_ldm(model, prompt: List[str], controller, num_inference_steps: in
     uncond = _encode(model, [""] * batch_size, model.bert)
     text = _encode(model, prompt, model.bert)
     latent, latents = init_latent(latent, model, height, width, generator, batch_size)
-    context = torch.cat([uncond, text])
+    context = unet_context(model, torch.cat([uncond, text]))
     model.scheduler.set_timesteps(num_inference_steps)
     for t in model.scheduler.timesteps:
         latents = diffusion_step(model, controller, latents, context, t, guidance_scale)
@@ -144,11 +157,16 @@ def text2image_ldm_stable(model, prompt: List[str], controller, num_inference_st
         uncond = None
     latent, latents = init_latent(latent, model, height, width, generator, batch_size)
     model.scheduler.set_timesteps(num_inference_steps)
+    # one context for the whole loop, as ptp_utils.py:158-160 builds it: the cross-attention K / V
+    # projections of an unchanged context are then computed once (_project's cache); per-step null
+    # embeddings make a new context every step
+    context = None if uncond_embeddings is not None else unet_context(
+        model, [uncond, text] if low_resource else torch.cat([uncond, text]))
     for i, t in enumerate(model.scheduler.timesteps):
         if uncond_embeddings is not None:
             u = uncond_embeddings[i] if isinstance(uncond_embeddings, (list, tuple)) else uncond_embeddings
             uncond = u.expand(*text.shape)
-        context = [uncond, text] if low_resource else torch.cat([uncond, text])
+            context = [uncond, text] if low_resource else torch.cat([uncond, text])
         latents = diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource)
     image = latent2image(model.vae, latents) if getattr(model, "vae", None) is not None else latents
     return image, latent
@@ -189,17 +207,42 @@ def _stacked_weight(module, names):
     return hit[1]
 
 
+CACHE_CROSS_KV = os.environ.get("P2P_CACHE_CROSS_KV", "1") != "0"
+
+
+def _cross_kv(module, context, w):
+    """linear(context, [to_k; to_v]) of a cross-attention, computed once per (context, weights):
+    the sampling loop hands every U-Net call of an edit group the same context tensor
+    (ptp_utils.py:158-168), so its K / V are the same at all 50 steps.  The cache holds the
+    context by identity (a weak reference: a new tensor, even at a recycled address, misses) and
+    its version counter (an in-place change misses), and the stacked weight object (rebuilt by
+    _stacked_weight whenever a projection weight changes).  Not cached: inference-mode tensors (no
+    version counter) and calls under stream capture (a graph replays its own GEMM on refilled
+    static inputs, e.g. null-text's per-step uncond embeddings)."""
+    import weakref
+    if (not CACHE_CROSS_KV or context.is_inference() or context.requires_grad
+            or (context.is_cuda and torch.cuda.is_current_stream_capturing())):
+        return torch.nn.functional.linear(context, w)
+    hit = module.__dict__.get("_p2p_kv")
+    if hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w:
+        return hit[3]
+    kv = torch.nn.functional.linear(context, w)
+    module.__dict__["_p2p_kv"] = (weakref.ref(context), context._version, w, kv)
+    return kv
+
+
 def _project(module, x, context, is_cross):
     """q, k, v of ptp_utils.py:186-193.  Outside autograd one GEMM produces them (x read once
     for self-attention, the context once for k and v) and the kernels read q/k/v as strided
-    views of its output -- no head split copies (``[b,n,h*d] -> [b*h,n,d]``, :191-193)."""
+    views of its output -- no head split copies (``[b,n,h*d] -> [b*h,n,d]``, :191-193).  A
+    cross-attention's k / v of an unchanged context come from the previous call (_cross_kv)."""
     src = context if is_cross else x
     grad = torch.is_grad_enabled() and (x.requires_grad or src.requires_grad)
     if FUSE_PROJECTIONS and not grad and x.is_cuda:
         if is_cross:
             w = _stacked_weight(module, ("to_k", "to_v"))
             if w is not None:
-                kv = torch.nn.functional.linear(src, w)
+                kv = _cross_kv(module, src, w)
                 C = kv.shape[-1] // 2
                 return module.to_q(x), kv[..., :C], kv[..., C:]
         else:

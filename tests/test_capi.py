@@ -103,6 +103,14 @@ def test_localblend_rejects():
     assert L.p2p_store_scale(None, None, 1.0, 10, None) == -1
 
 
+def test_clock_probe_rejects():
+    L = _hip.lib()
+    assert L.p2p_clock_probe(None, 8, 1000, None) == -1
+    assert L.p2p_clock_probe(64, 0, 1000, None) == -1
+    assert L.p2p_clock_probe(64, 8, 0, None) == -1
+    assert L.p2p_clock_probe(64, 2048, 1000, None) == -1
+
+
 def test_cross_attn_rejects_program_with_too_few_edits():
     """a group of 4 prompts needs a program with >= 3 edit records; one built for fewer
     would make the kernel read past the program blob and the alpha row."""

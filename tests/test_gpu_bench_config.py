@@ -62,9 +62,12 @@ def _record_oracle_masks(olb, sink):
     return Rec()
 
 
-def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
+def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3), unet_dtype=torch.bfloat16, compute="bf16",
+                            run_bars=(0.99, 0.95), negatives=True):
+    """run_bars: (mean, per-step minimum) of the product's partial masks against the oracle's OWN
+    run (all-ones masks: 0.999 at every step)."""
     prompts = pl.north_star_prompts()
-    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=unet_dtype)
     if gain != 1.0:
         sharpen_attention(model, gain)
     x_T = pl.seed_latent(0)
@@ -72,7 +75,7 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
     pmasks, fmasks = [], []
     flb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok, th=th)
     flb.alpha = flb.alpha.to(cuda)
-    with config.compute_mode("bf16"):
+    with config.compute_mode(compute):
         ctrl = pl.make_replace_controller(prompts, 50, device=cuda, blend_th=th)
         _record_masks(ctrl.local_blend, pmasks, fmasks, flb)
         got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
@@ -84,7 +87,8 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
     print("product run done", flush=True)
     want = oracle_group(model, prompts, x_T, octrl, 50)
     cos = cosine(got, want)
-    print(f"bench config (bf16 U-Net + bf16 kernels, attention gain {gain}) final-latent cosine per prompt:",
+    print(f"bench config ({str(unet_dtype)[6:]} U-Net + {compute} kernels, attention gain {gain}) final-latent "
+          "cosine per prompt:",
           [round(c, 6) for c in cos.tolist()])
     assert torch.isfinite(got).all()
     assert cos.min().item() >= 0.999, cos
@@ -103,16 +107,23 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
           f"{min(forced):.6f}; edit-prompt mask coverage {min(cover):.3f}..{max(cover):.3f}")
     assert n == 40
     # north star: >= 99.9 % of the pixels at EVERY step where both sides see the same maps.  Across
-    # the two bf16 trajectories a partial mask (coverage < 1, the sharpened run) moves by whole 4x4
+    # two bf16 U-Net trajectories a partial mask (coverage < 1, the sharpened run) moves by whole 4x4
     # blocks of the 16x16 maps wherever a map value sits near its threshold, so there the run-vs-run
-    # agreement is held to 98 % on average and 95 % per step (measured 99.3 % / 96.9 %; all-ones
-    # masks: 99.9 % every step)
+    # agreement is held to run_bars (bf16 U-Net: 99 % on average and 95 % per step; logged 99.50 /
+    # 99.60 % mean, 96.7-98.0 % minimum: profiles/r05/evidence_r05h, evidence_r05n).  With the f32
+    # U-Net the U-Net's own rounding is out of the picture and the bar is the north star's 99.9 %.
     print("  per-step agreement vs the oracle's run:", [round(x, 4) for x in agree])
     assert min(forced) >= 0.999, forced
     if min(cover) == 1.0:
         assert min(agree) >= 0.999, agree
     else:
-        assert sum(agree) / n >= 0.98 and min(agree) >= 0.95, agree
+        assert sum(agree) / n >= run_bars[0] and min(agree) >= run_bars[1], agree
+        if min(agree) < 1.0:
+            _explain_flips(pmasks, omasks, agree)
+    if not negatives:
+        check_effect(f"configs[1], {str(unet_dtype)[6:]} U-Net + {compute} kernels, gain {gain}", got, want,
+                     base_group(model, prompts, x_T, 50), effect_bar)
+        return
     # the edit's effect, and negative controls that must fail the same bar
     base = base_group(model, prompts, x_T, 50)
     check_effect(f"configs[1] as benched, gain {gain}", got, want, base, effect_bar)
@@ -134,6 +145,19 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3)):
         check_negative("LocalBlend off", neg_blend, want, base, effect_bar)
 
 
+def _explain_flips(pmasks, omasks, agree):
+    """For the worst step: how many pixels and 16x16 map cells (4x4 pixel blocks after the nearest
+    upsample) differ between the product's and the oracle's run, per prompt."""
+    i = min(range(len(agree)), key=lambda j: agree[j])
+    steps = [j for j, m in enumerate(pmasks) if m is not None]
+    s = steps[i]
+    pm, om = pmasks[s] != 0, omasks[s].reshape(pmasks[s].shape)
+    diff = (pm != om)
+    cells = diff[:, 0].reshape(diff.shape[0], 16, 4, 16, 4).any(4).any(2)
+    print(f"  worst step {s}: {int(diff.sum())} pixels = {int(cells.sum())} of {cells.numel()} 16x16 cells differ "
+          f"(per prompt {cells.flatten(1).sum(1).tolist()})", flush=True)
+
+
 def test_bench_default_config_50_steps(cuda, tok):
     """configs[1] exactly as benched (random-init weights).  The edit moves the latents by ~2 % of
     their norm here and the two bf16 trajectories differ by ~0.8 %, so the edit-effect bar is 0.70
@@ -152,6 +176,20 @@ def test_bench_config_sharpened_50_steps(cuda, tok):
     moves whole blocks of an edit's latent between its own and the source's values: the effect
     bar is 0.97 here (measured 0.983-0.998; LocalBlend-off, the nearest negative, 0.77-0.84)."""
     _bench_config_vs_oracle(cuda, tok, 4.0, 0.97, th=(0.8, 0.8))
+
+
+@pytest.mark.parametrize("compute, run_bars", [("f32", (0.999, 0.999)), ("bf16", (0.999, 0.995))], ids=["f32", "bf16"])
+def test_bench_config_f32unet_sharpened_partial_masks(cuda, tok, compute, run_bars):
+    """LocalBlend end to end on PARTIAL masks with the U-Net's rounding out of the picture: configs[1]
+    (1 source + 3 Replace edits, null_text LocalBlend, 50 DDIM steps) on an f32 U-Net, sharpened
+    (every logit x4) with thresholds 0.8, so the masks cover about half the pixels, against the
+    oracle's own fp32 run (null_text.py:41-70, main.py:164-167).  North-star bar: the masks agree on
+    >= 99.9 % of the pixels -- at every blended step in the f32 check mode, on average (per-step
+    minimum >= 99.5 %) with the bf16 kernels, whose probabilities sit within 2e-3 of the oracle's
+    and can move a 16x16 map cell that lies that close to its threshold (one cell = 16 of the 4 x
+    64 x 64 pixels = 0.1 %).  Edit-effect bar 0.99 (f32 U-Net)."""
+    _bench_config_vs_oracle(cuda, tok, 4.0, EFFECT_BAR, th=(0.8, 0.8), unet_dtype=torch.float32, compute=compute,
+                            run_bars=run_bars, negatives=False)
 
 
 STEPS2 = 10

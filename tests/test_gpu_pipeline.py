@@ -90,3 +90,44 @@ def test_edit_group_check_mode_tight(cuda, tok):
     cos = cosine(got, want)
     print("check-mode final-latent cosine:", [round(c, 8) for c in cos.tolist()])
     assert cos.min().item() >= 0.99999, cos
+
+
+def test_cross_kv_cache_bit_identical(cuda):
+    """The cross-attention K / V projections are computed once per edit group (ptp_utils._cross_kv:
+    the loop's context is one tensor for all steps, ptp_utils.py:158-168): a bf16 edit group with
+    the cache is bit-identical to one that recomputes them at every call, the cached K / V equal a
+    fresh projection of the context, and the cache really served the later steps."""
+    from p2p_amd import ptp_utils as pu
+    prompts = pl.north_star_prompts()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    x_T = pl.seed_latent(5)
+    steps = 6
+    calls = []
+    orig = pu._cross_kv
+
+    fresh_equal = []
+
+    def counting(module, context, w):
+        hit = module.__dict__.get("_p2p_kv")
+        calls.append(hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w)
+        kv = orig(module, context, w)
+        if calls[-1]:   # a cached K / V against a fresh projection of the same context
+            fresh_equal.append(torch.equal(kv, torch.nn.functional.linear(context, w)))
+        return kv
+    pu._cross_kv = counting
+    try:
+        with config.compute_mode("bf16"):
+            got = pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
+                                    num_steps=steps)
+            pu.CACHE_CROSS_KV = False
+            want = pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
+                                     num_steps=steps)
+    finally:
+        pu._cross_kv = orig
+        pu.CACHE_CROSS_KV = True
+    n_cross = 16
+    assert len(calls) == 2 * steps * n_cross
+    # cache on: the first U-Net call of the group computes, the other steps hit
+    assert calls[:n_cross] == [False] * n_cross and all(calls[n_cross:steps * n_cross]), calls[:steps * n_cross]
+    assert len(fresh_equal) == (steps - 1) * n_cross and all(fresh_equal)
+    assert torch.equal(got, want)

@@ -235,3 +235,61 @@ def test_cross_step_plan(tok):
     rep.cur_step = 0
     rep.cross_replace_alpha.zero_()
     assert rep._cross_step(torch.device("cpu"), 77)[0] is None
+    # a controller built under torch.inference_mode(): its alpha table has no version counter
+    with torch.inference_mode():
+        inf = pc.AttentionReplace(prompts, 10, 0.8, 0.4, tokenizer=tok, device=torch.device("cpu"))
+        assert inf.cross_replace_alpha.is_inference()
+        got = []
+        for step in range(10):
+            inf.cur_step = step
+            prog, hints = inf._cross_step(torch.device("cpu"), 77)
+            got.append(("plain" if prog is None else "r_only" if hints == _hip.GROUP_F_R_ONLY else "edit"))
+    assert got == plans, got
+
+
+def test_cross_kv_cache_rules():
+    """ptp_utils._cross_kv: the cross-attention K / V of an unchanged context are computed once
+    (ptp_utils.py:158-168 hands every step the same context); a new context object -- even with
+    equal contents or at a recycled address --, an in-place change of the context, a rebuilt
+    stacked weight and an inference-mode context all recompute."""
+    from p2p_amd import ptp_utils as pu
+
+    class M:
+        pass
+    m = M()
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(16, 8, generator=g)
+    ctx = torch.randn(2, 5, 8, generator=g)
+    calls = []
+    orig = torch.nn.functional.linear
+
+    def counting(x, weight, bias=None):
+        calls.append(1)
+        return orig(x, weight, bias)
+    torch.nn.functional.linear = counting
+    try:
+        a = pu._cross_kv(m, ctx, w)
+        b = pu._cross_kv(m, ctx, w)
+        assert b is a and len(calls) == 1
+        assert torch.equal(a, orig(ctx, w))
+        ctx.mul_(2.0)                              # in place: the version counter moves
+        c = pu._cross_kv(m, ctx, w)
+        assert len(calls) == 2 and torch.equal(c, orig(ctx, w))
+        other = ctx.clone()                        # equal contents, another tensor
+        pu._cross_kv(m, other, w)
+        assert len(calls) == 3
+        w2 = w.clone()                             # a rebuilt stacked weight
+        pu._cross_kv(m, other, w2)
+        assert len(calls) == 4
+        with torch.inference_mode():
+            inf = torch.randn(2, 5, 8)
+            pu._cross_kv(m, inf, w)
+            pu._cross_kv(m, inf, w)
+        assert len(calls) == 6
+        pu.CACHE_CROSS_KV = False
+        pu._cross_kv(m, other, w2)
+        pu._cross_kv(m, other, w2)
+        assert len(calls) == 8
+    finally:
+        torch.nn.functional.linear = orig
+        pu.CACHE_CROSS_KV = True

@@ -19,6 +19,9 @@
 #     stamps:<tool>:<v>      a clock-stamp tool (tools/<tool>.py) under P2P_SELF_VARIANT=v (experiments lib)
 #     pmcs:<tag>:<script>:<args>  tools/gpu_pmc.sh over any launcher script (comma-separated args)
 #     py:<script>[:<a1,a2,..>]  python -u <script> <a1> <a2> ..
+#     g1shape:<v>:<P,d>      tools/g1_ab.py (correctness + isolated timing) of variant v at shape P,d (experiments lib)
+#     variants:<v1,v2,..>[:<prefix>]  in-pipeline A/B: a short bench.py per P2P_SELF_VARIANT (experiments lib),
+#                            printing the HIP-event average of every attention geometry (starting with <prefix>)
 set -u
 export TMPDIR=/tmp
 tag=$1; shift
@@ -82,6 +85,19 @@ for step in "$@"; do
       script=${arg%%:*}; sargs=""; [ "$script" != "$arg" ] && sargs=${arg#*:}
       run 1100 "$out/py_$(basename "$script" .py).log" python -u "$script" ${sargs//,/ }
       tail -15 "$out/py_$(basename "$script" .py).log" ;;
+    g1shape)
+      v=${arg%%:*}; shape=${arg#*:}
+      run 150 "$out/g1shape_$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v G1AB_SHAPE=$shape python -u tools/g1_ab.py
+      tail -1 "$out/g1shape_$v.log" ;;
+    variants)
+      vs=${arg%%:*}; prefix=""; [ "$vs" != "$arg" ] && prefix=${arg#*:}
+      for v in ${vs//,/ }; do
+        run 600 "$out/variant_$v.log" env P2P_EXPERIMENTS_LIB=1 P2P_SELF_VARIANT=$v python -u bench.py --gpus 1 --steps 4 --warmup 2 --no-cpu-baseline
+        grep '^{' "$out/variant_$v.log" | tail -1 | python3 -c "
+import json, sys; d = json.loads(sys.stdin.read())
+print('variant $v', round(d['value'], 4), [(g['geometry'], round(g['avg_launch_ms'] * 1e3, 1))
+      for g in d['roofline_attn_total']['by_geometry'] if g['geometry'].startswith('$prefix')])" | tee -a "$out/variants.txt"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

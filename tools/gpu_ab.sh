@@ -6,9 +6,10 @@
 set -u
 cd "$(dirname "$0")/.."
 make -C prompt-to-prompt_amd/csrc EXPERIMENTS=1 -j8 > /tmp/make_exp.log 2>&1 || { tail -20 /tmp/make_exp.log; exit 1; }
-cp .gpurunignore /tmp/gpurunignore.bak
-grep -v '^\./prompt-to-prompt_amd/p2p_amd/exp$' /tmp/gpurunignore.bak > .gpurunignore
+bak=$(mktemp /tmp/gpurunignore.XXXXXX)
+cp .gpurunignore "$bak"
+# restore the tracked file however this script ends (error, Ctrl-C, kill)
+trap 'cp "$bak" .gpurunignore; rm -f "$bak"' EXIT
+trap 'exit 130' INT TERM
+grep -v '^\./prompt-to-prompt_amd/p2p_amd/exp$' "$bak" > .gpurunignore
 /usr/local/graft/bin/gpurun "$@"
-rc=$?
-cp /tmp/gpurunignore.bak .gpurunignore
-exit $rc
