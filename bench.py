@@ -68,11 +68,11 @@ class FenceFreeEvent:
             cls._hip = L
         return cls._hip
 
-    def __init__(self):
+    def __init__(self, flags=0x20000000):   # hipEventDisableSystemFence
         import ctypes
         self._ctypes = ctypes
         self.ev = ctypes.c_void_p()
-        rc = self._lib().hipEventCreateWithFlags(ctypes.byref(self.ev), 0x20000000)   # hipEventDisableSystemFence
+        rc = self._lib().hipEventCreateWithFlags(ctypes.byref(self.ev), flags)
         if rc != 0:
             raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
 
@@ -159,9 +159,12 @@ class LaunchTimer:
     Every record also carries the index of the batch (edit group) it ran in, so per-batch
     averages show clock droop over a long run."""
 
-    def __init__(self, n_query=4096, fence_free=True):
+    def __init__(self, n_query=4096, mode="ext"):
         self.n_query = n_query
-        self.event = FenceFreeEvent if fence_free else (lambda: torch.cuda.Event(enable_timing=True))
+        # "ext": the kernels' own dispatch timestamps (p2p_set_launch_events -> hipExtLaunchKernel; no
+        # marker packets between the launches); "fence-free" / "torch": events recorded around the call
+        self.mode = mode
+        self.event = FenceFreeEvent if mode != "torch" else (lambda: torch.cuda.Event(enable_timing=True))
         self.rec = {}            # name -> list of (start event, end event, work, batch)
         self._pending = None     # (start event, [(name, work), ...])
         self.enabled = False
@@ -194,17 +197,30 @@ class LaunchTimer:
         if not self.enabled:
             return
         info = info or {"stored": 0, "accumulate": False}
-        ev = self.event()
-        ev.record()
-        self._pending = (ev, self._names(kind, t, info))
+        self._open(self._names(kind, t, info))
         if kind == "cross" and "n_groups" in info:
             self.cross_group_kernel[f"attn:cross:P{t.n_query}:d{t.head_dim}"] = bool(info.get("group_kernel"))
 
-    def after(self, kind, t, info=None):
-        if self._pending is not None:
+    def _open(self, names):
+        if self.mode == "ext":
+            from p2p_amd import _hip
+            start, stop = FenceFreeEvent(flags=0), FenceFreeEvent(flags=0)
+            _hip.lib().p2p_set_launch_events(start.ev, stop.ev)
+            self._pending = (start, names, stop)
+        else:
             ev = self.event()
             ev.record()
-            start, names = self._pending
+            self._pending = (ev, names, None)
+
+    def after(self, kind, t, info=None):
+        if self._pending is not None:
+            start, names, ev = self._pending
+            if ev is not None:
+                from p2p_amd import _hip
+                _hip.lib().p2p_set_launch_events(None, None)
+            else:
+                ev = self.event()
+                ev.record()
             for name, work in names:
                 self.rec.setdefault(name, []).append((start, ev, work, self.batch))
             self._pending = None
@@ -214,9 +230,7 @@ class LaunchTimer:
     def before_aux(self, name, nbytes):
         """The LocalBlend mask and latent-step launches (HBM-type helpers), with their bytes."""
         if self.enabled:
-            ev = self.event()
-            ev.record()
-            self._pending = (ev, [(name, float(nbytes))])
+            self._open([(name, float(nbytes))])
 
     def after_aux(self, name):
         self.after(name, None)
@@ -232,20 +246,31 @@ class LaunchTimer:
         """(average ms per launch, average work per launch, launches)"""
         torch.cuda.synchronize()
         pairs = [r for r in self.rec.get(name, []) if batch is None or r[3] == batch]
+        pairs = [(r, self._ms(r)) for r in pairs]
+        pairs = [(r, ms) for r, ms in pairs if ms is not None]
         if not pairs:
             return None, None, 0
-        ms = [a.elapsed_time(b) for a, b, _, _ in pairs]
-        return sum(ms) / len(ms), sum(w for _, _, w, _ in pairs) / len(pairs), len(ms)
+        return (sum(ms for _, ms in pairs) / len(pairs), sum(r[2] for r, _ in pairs) / len(pairs), len(pairs))
+
+    @staticmethod
+    def _ms(r):
+        """One record's launch time; None for a bracket whose call launched no kernel (ext events
+        never bound)."""
+        try:
+            return r[0].elapsed_time(r[1])
+        except RuntimeError:
+            return None
 
     def attn_total(self, peak, unet_calls):
         """Aggregate roofline of ALL attention launches: summed algorithmic FLOP / summed HIP-event
         time, and the per-geometry split (average launch, its FLOP and fraction of peak)."""
         torch.cuda.synchronize()
-        recs = self.rec.get("attn", [])
+        recs = [(r, self._ms(r)) for r in self.rec.get("attn", [])]
+        recs = [(r, ms) for r, ms in recs if ms is not None]
         if not recs:
             return None
-        tot_ms = sum(a.elapsed_time(b) for a, b, _, _ in recs)
-        tot_flop = sum(w for _, _, w, _ in recs)
+        tot_ms = sum(ms for _, ms in recs)
+        tot_flop = sum(r[2] for r, _ in recs)
         achieved = tot_flop / (tot_ms * 1e-3) / 1e12
         by = []
         kind_ms, kind_flop, kind_bytes = {}, {}, {}
@@ -416,9 +441,10 @@ def main():
     ap.add_argument("--unet-dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--compute", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--launch-events", default="fence-free", choices=["fence-free", "torch"],
-                    help="per-launch timing events: HIP events without the system-scope fence (default) or\n"
-                         "torch.cuda.Event (an L2 writeback + invalidate at every record)")
+    ap.add_argument("--launch-events", default="ext", choices=["ext", "fence-free", "torch"],
+                    help="per-launch timing: the kernels' own dispatch timestamps through hipExtLaunchKernel\n"
+                         "events (default; p2p_set_launch_events), HIP events recorded around each call without\n"
+                         "the system-scope fence, or torch.cuda.Event (an L2 writeback + invalidate per record)")
     ap.add_argument("--groups-per-call", type=int, default=1,
                     help="edit groups denoised per U-Net call (controllers.GroupBatch; a step = one such\n"
                          "batch); 1 = configs[1] as quoted")
@@ -462,7 +488,7 @@ def main():
     model = pl.SyntheticStableDiffusion(device=dev, dtype=dtype)
     prompts = pl.north_star_prompts()
     B = len(prompts)
-    timer = LaunchTimer(fence_free=args.launch_events == "fence-free")
+    timer = LaunchTimer(mode=args.launch_events)
     _hip.LAUNCH_OBSERVER = timer
 
     G = args.groups_per_call
@@ -537,8 +563,12 @@ def main():
                     "avg_launch_ms": avg_ms, "launches": n_launch,
                     "flop_per_launch": flops,
                     **_clock_fields(clock.summary(), (achieved / peak) if achieved else None),
-                    "timing": ("HIP events around each launch on its stream, created with hipEventDisableSystemFence"
-                               if args.launch_events == "fence-free" else "torch.cuda.Event around each launch")}
+                    "timing": {"ext": "HIP events bound to each launch's kernels (hipExtLaunchKernel start / stop "
+                                      "events: the kernels' own dispatch timestamps, as rocprofv3's kernel trace), "
+                                      "on the launch stream",
+                               "fence-free": "HIP events recorded around each launch on its stream, created with "
+                                             "hipEventDisableSystemFence",
+                               "torch": "torch.cuda.Event around each launch"}[args.launch_events]}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.ddim_steps)

@@ -253,6 +253,12 @@ int p2p_store_scale(const float* src, float* dst, float divisor, int64_t n, p2p_
  * memory, 2 x n_workgroups (1..1024) u64. */
 int p2p_clock_probe(uint64_t* out, int32_t n_workgroups, int32_t ticks, p2p_stream_t stream);
 
+/* Measurement only (ABI 15): kernel timing events (hipEvent_t, created by the caller) for the
+ * next p2p_* calls of the calling thread -- their kernels are launched with hipExtLaunchKernel,
+ * the first one recording `start`, each one `stop` (the last kernel's stands), from the kernels'
+ * own dispatch timestamps.  Clear with (NULL, NULL).  Always returns 0. */
+int p2p_set_launch_events(void* start, void* stop);
+
 /* Build/runtime information.  p2p_source_hash: content hash of the HIP sources the library
  * was built from (p2p_amd/_srchash.py), so a host can refuse a stale prebuilt binary. */
 int p2p_abi_version(void);

@@ -1879,15 +1879,15 @@ static void launch_fused(const SelfArgs& a, hipStream_t st) {
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
   constexpr bool kOnes = ((D + 31) / 32 * 32) > D;
   if (a.n_maps > 0)  // the lse feeds stored maps: exact f32 row sums
-    hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
+    launch_kernel((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, true>), grid, block, 0, st, b);
   else if constexpr (kOnes && MP::kElemBytes == 2) {
     // O only (no lse): no per-tile max
     if (a.lse == nullptr)
-      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false, true>), grid, block, 0, st, b);
+      launch_kernel((self_attn_fused_kernel<IO, MQ, MP, D, BK, W, false, true>), grid, block, 0, st, b);
     else
-      hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+      launch_kernel((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
   } else
-    hipLaunchKernelGGL((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
+    launch_kernel((self_attn_fused_kernel<IO, MQ, MP, D, BK, W>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, int D, int BK, int W, int QB, bool F16 = false, bool PIPE = false,
@@ -1896,7 +1896,7 @@ static void launch_multi(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W * QB - 1) / (32 * W * QB);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16, PIPE, PRIO>), grid, block, 0, st, b);
+  launch_kernel((self_attn_multi_kernel<IO, MQ, D, BK, W, QB, F16, PIPE, PRIO>), grid, block, 0, st, b);
 }
 
 template <typename IO, typename MQ, typename MP, int D>
@@ -1949,7 +1949,7 @@ static hipError_t launch_self_d(const SelfArgs& a, int mode, hipStream_t st) {
   constexpr int W = 4;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_pv_kernel<IO, MP, D, BK, W>), grid, block, 0, st, b);
+  launch_kernel((self_pv_kernel<IO, MP, D, BK, W>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -1971,19 +1971,19 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
 #ifdef P2P_EXPERIMENTS
   if (dense && a.variant == 201 && D > 80) {
-    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 201>), grid, block, dyn, st, b);
+    launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 201>), grid, block, dyn, st, b);
     return hipGetLastError();
   }
   if (a.variant == 202) {
-    if (dense) hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 202>), grid, block, dyn, st, b);
-    else hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false, 202>), grid, block, dyn, st, b);
+    if (dense) launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 202>), grid, block, dyn, st, b);
+    else launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, false, 202>), grid, block, dyn, st, b);
     return hipGetLastError();
   }
 #endif
   if (dense)
-    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
+    launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
   else
-    hipLaunchKernelGGL((cross_attn_kernel<IO, MQ, MP, D, W, false>), grid, block, dyn, st, b);
+    launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, false>), grid, block, dyn, st, b);
   return hipGetLastError();
 }
 
@@ -2015,7 +2015,7 @@ static hipError_t launch_self_maps_d(const SelfArgs& a, hipStream_t st) {
   dim3 grid(n_kgroups * b.n_qtiles * a.H * a.n_maps), block(256);
   // non-temporal running-sum accesses (the map streams through once per step: -7.5 % at G2 with
   // the maps HBM-resident; two key blocks per step measured +2 %, not instantiated)
-  hipLaunchKernelGGL((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
+  launch_kernel((self_maps_kernel<IO, MQ, D, 1, true>), grid, block, 0, st, b, kw, n_kgroups);
   return hipGetLastError();
 }
 
@@ -2026,7 +2026,7 @@ static hipError_t launch_self_probs_d(const SelfArgs& a, hipStream_t st) {
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(b.n_qtiles * a.H * a.N), block(256);
   // non-temporal probability stores (a write-once stream: G1 1.33 -> 1.04 ms, G2 118 -> 104 us)
-  hipLaunchKernelGGL((self_probs_kernel<IO, MQ, D, true>), grid, block, 0, st, b, kw);
+  launch_kernel((self_probs_kernel<IO, MQ, D, true>), grid, block, 0, st, b, kw);
   return hipGetLastError();
 }
 

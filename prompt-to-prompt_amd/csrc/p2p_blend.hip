@@ -475,17 +475,17 @@ int run_latent_step(const p2p_latent_step_args& a, hipStream_t st) {
     const int hw = a.height * a.width;
     dim3 grid((hw + kPx - 1) / kPx, a.n_prompts);
     if (a.eps_dtype == P2P_DTYPE_BF16)
-      hipLaunchKernelGGL(latent_blend_kernel<true>, grid, dim3(256), 0, st, a, chw, kPx);
+      launch_kernel(latent_blend_kernel<true>, grid, dim3(256), 0, st, a, chw, kPx);
     else
-      hipLaunchKernelGGL(latent_blend_kernel<false>, grid, dim3(256), 0, st, a, chw, kPx);
+      launch_kernel(latent_blend_kernel<false>, grid, dim3(256), 0, st, a, chw, kPx);
     return (int)hipGetLastError();
   }
   int64_t blocks = (chw + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (a.eps_dtype == P2P_DTYPE_BF16)
-    hipLaunchKernelGGL(latent_step_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
+    launch_kernel(latent_step_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
   else
-    hipLaunchKernelGGL(latent_step_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
+    launch_kernel(latent_step_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a, chw);
   return (int)hipGetLastError();
 }
 
@@ -497,13 +497,13 @@ int run_localblend(const p2p_blend_args& a, hipStream_t st) {
   for (int l = 0; l < a.n_maps; ++l)
     if (!a.maps[l] && !a.word_sums_ready) return P2P_E_ARG;
   dim3 g1(a.n_prompts, a.n_maps * a.heads_per_map, (a.map_res * a.map_res + kWsPix - 1) / kWsPix);
-  if (!a.word_sums_ready) hipLaunchKernelGGL(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
-  hipLaunchKernelGGL(blend_finalize_kernel, dim3(a.n_prompts), dim3(256), 0, st, a);
+  if (!a.word_sums_ready) launch_kernel(blend_wordsum_kernel, g1, dim3(256), 0, st, a);
+  launch_kernel(blend_finalize_kernel, dim3(a.n_prompts), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
 int run_clock_probe(unsigned long long* out, int n_wg, int ticks, hipStream_t st) {
-  hipLaunchKernelGGL(clock_probe_kernel, dim3((unsigned)n_wg), dim3(64), 0, st, out, (unsigned)ticks);
+  launch_kernel(clock_probe_kernel, dim3((unsigned)n_wg), dim3(64), 0, st, out, (unsigned)ticks);
   return (int)hipGetLastError();
 }
 
@@ -514,7 +514,7 @@ int run_store_scale(const float* src, float* dst, float divisor, int64_t n, hipS
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
   const float inv = 1.0f / divisor;
-  hipLaunchKernelGGL(store_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, inv, n);
+  launch_kernel(store_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, inv, n);
   return (int)hipGetLastError();
 }
 

@@ -353,7 +353,7 @@ static void launch_dkv(const BwdArgs& a, hipStream_t st) {
   BwdArgs b = a;
   b.n_tiles = (a.K + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_tiles * a.N * a.H * a.kv_split), block(64 * W);
-  hipLaunchKernelGGL((bwd_dkv_kernel<IO, OUT, D, T, W, WANT>), grid, block, 0, st, b);
+  launch_kernel((bwd_dkv_kernel<IO, OUT, D, T, W, WANT>), grid, block, 0, st, b);
 }
 
 constexpr int kBwdWaves = 4;
@@ -387,7 +387,7 @@ static void launch_kv_out(const BwdArgs& a, hipStream_t st) {
     const int64_t n4 = (int64_t)a.N * a.K * a.H * D / 4;
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((bwd_kv_reduce_kernel<OUT>), dim3((unsigned)blocks), dim3(256), 0, st, a, n4);
+    launch_kernel((bwd_kv_reduce_kernel<OUT>), dim3((unsigned)blocks), dim3(256), 0, st, a, n4);
   }
 }
 
@@ -396,11 +396,11 @@ static int launch_bwd_d(BwdArgs a, hipStream_t st) {
   constexpr int T = BwdTile<D>::T;
   constexpr int W = kBwdWaves;
   const int64_t nd = (int64_t)a.N * a.H * a.P;
-  hipLaunchKernelGGL((bwd_delta_kernel<IO, D>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, a);
+  launch_kernel((bwd_delta_kernel<IO, D>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, a);
   {
     BwdArgs b = a;
     b.n_tiles = (a.P + 32 * W - 1) / (32 * W);
-    hipLaunchKernelGGL((bwd_dq_kernel<IO, D, T, W>), dim3(b.n_tiles * a.N * a.H), dim3(64 * W), 0, st, b);
+    launch_kernel((bwd_dq_kernel<IO, D, T, W>), dim3(b.n_tiles * a.N * a.H), dim3(64 * W), 0, st, b);
   }
   // key/value pass: split the queries when the key tiles alone leave the chip idle
   a.kv_split = kv_split_for(a.N, a.H, a.P, a.K, T);

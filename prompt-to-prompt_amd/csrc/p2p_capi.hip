@@ -66,7 +66,21 @@ int self_variant() { return kSelfVariant; }
 
 }  // namespace
 
+namespace p2p {
+LaunchEvents& launch_events() {
+  static thread_local LaunchEvents ev;
+  return ev;
+}
+}  // namespace p2p
+
 extern "C" {
+
+int p2p_set_launch_events(void* start, void* stop) {
+  LaunchEvents& ev = launch_events();
+  ev.start = static_cast<hipEvent_t>(start);
+  ev.stop = static_cast<hipEvent_t>(stop);
+  return 0;
+}
 
 int p2p_abi_version(void) { return P2P_ABI_VERSION; }
 

@@ -555,17 +555,17 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   dim3 grid(b.n_qtiles * a.H * a.n_groups), block(64 * W);
 #ifdef P2P_EXPERIMENTS
   if (a.variant == 202) {
-    if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true, 202>), grid, block, dyn, st, b);
-    else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false, 202>), grid, block, dyn, st, b);
-    else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true, 202>), grid, block, dyn, st, b);
-    else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false, 202>), grid, block, dyn, st, b);
+    if (edit && store) launch_kernel((cross_group_kernel<D, W, true, true, 202>), grid, block, dyn, st, b);
+    else if (edit) launch_kernel((cross_group_kernel<D, W, true, false, 202>), grid, block, dyn, st, b);
+    else if (store) launch_kernel((cross_group_kernel<D, W, false, true, 202>), grid, block, dyn, st, b);
+    else launch_kernel((cross_group_kernel<D, W, false, false, 202>), grid, block, dyn, st, b);
     return hipGetLastError();
   }
 #endif
-  if (edit && store) hipLaunchKernelGGL((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
-  else if (edit) hipLaunchKernelGGL((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
-  else if (store) hipLaunchKernelGGL((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
-  else hipLaunchKernelGGL((cross_group_kernel<D, W, false, false>), grid, block, dyn, st, b);
+  if (edit && store) launch_kernel((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
+  else if (edit) launch_kernel((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
+  else if (store) launch_kernel((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
+  else launch_kernel((cross_group_kernel<D, W, false, false>), grid, block, dyn, st, b);
   return hipGetLastError();
 }
 

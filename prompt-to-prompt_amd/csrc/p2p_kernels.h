@@ -1,12 +1,35 @@
 // Kernel-argument structs shared by the kernels and the C-ABI shim (passed by value).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/p2p_hip.h"
 
 namespace p2p {
+
+// Kernel timing events of the calling thread (p2p_set_launch_events, ABI 15; measurement only):
+// while set, launches go through hipExtLaunchKernel, which records the events from the kernel's own
+// dispatch -- the first kernel of a C-ABI call takes `start`, every kernel takes `stop` (the last
+// one's stands) -- instead of extra marker packets queued around the call.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& launch_events();
+
+template <typename F, typename... Args>
+inline void launch_kernel(F kernel, const dim3& grid, const dim3& block, uint32_t shmem, hipStream_t st,
+                          Args... args) {
+  LaunchEvents& ev = launch_events();
+  if (!ev.start && !ev.stop) {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, st, args...);
+    return;
+  }
+  hipEvent_t start = ev.start;
+  ev.start = nullptr;
+  hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, start, ev.stop, 0u, args...);
+}
 
 struct SelfArgs {
   const void* q;

@@ -662,7 +662,7 @@ hipError_t launch(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * QB * WAVES - 1) / (32 * QB * WAVES);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * WAVES);
-  hipLaunchKernelGGL((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
+  launch_kernel((self40_kernel<D, WAVES, QB, BK, SCHED, FORM>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 

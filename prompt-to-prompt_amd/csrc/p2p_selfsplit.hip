@@ -503,7 +503,7 @@ hipError_t launch_split(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 31) / 32;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_split_kernel<D, W, KBW>), grid, block, 0, st, b);
+  launch_kernel((self_split_kernel<D, W, KBW>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -512,7 +512,7 @@ hipError_t launch_ring(const SelfArgs& a, hipStream_t st) {
   SelfArgs b = a;
   b.n_qtiles = (a.P + 32 * W - 1) / (32 * W);
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-  hipLaunchKernelGGL((self_ring_kernel<160, W>), grid, block, 0, st, b);
+  launch_kernel((self_ring_kernel<160, W>), grid, block, 0, st, b);
   return hipGetLastError();
 }
 
@@ -533,7 +533,7 @@ int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
     SelfArgs b = a;
     b.n_qtiles = (a.P + 63) / 64;
     dim3 grid(b.n_qtiles * a.H * a.N), block(256);
-    hipLaunchKernelGGL(self_halves_kernel, grid, block, 0, st, b);
+    launch_kernel(self_halves_kernel, grid, block, 0, st, b);
     return (int)hipGetLastError();
   }
   return (int)launch_ring<4>(a, st);

@@ -114,9 +114,10 @@ def lib():
         L.p2p_attn_bwd_workspace.argtypes = [ctypes.POINTER(AttnTensors)]
         L.p2p_attn_bwd_workspace.restype = ctypes.c_int64
         L.p2p_clock_probe.argtypes = [vp, i32, i32, vp]
+        L.p2p_set_launch_events.argtypes = [vp, vp]
         for fn in ("p2p_self_attn_fwd", "p2p_cross_attn_fwd", "p2p_attn_probs", "p2p_attn_pv",
                    "p2p_localblend", "p2p_store_scale", "p2p_latent_step", "p2p_attn_fwd_lse", "p2p_attn_bwd",
-                   "p2p_clock_probe"):
+                   "p2p_clock_probe", "p2p_set_launch_events"):
             getattr(L, fn).restype = ctypes.c_int
         if L.p2p_abi_version() != ABI_VERSION:
             raise HipError(f"libp2p_hip.so ABI {L.p2p_abi_version()} != {ABI_VERSION}")
@@ -141,7 +142,8 @@ def check_source_hash() -> str:
 
 EXPORTED_SYMBOLS = ("p2p_abi_version", "p2p_source_hash", "p2p_error_string", "p2p_self_attn_fwd", "p2p_cross_attn_fwd",
                     "p2p_attn_probs", "p2p_attn_pv", "p2p_localblend", "p2p_store_scale", "p2p_latent_step",
-                    "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace", "p2p_clock_probe")
+                    "p2p_attn_fwd_lse", "p2p_attn_bwd", "p2p_attn_bwd_workspace", "p2p_clock_probe",
+                    "p2p_set_launch_events")
 
 
 def clock_probe(out: torch.Tensor, ticks: int = 1000):

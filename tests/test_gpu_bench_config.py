@@ -34,10 +34,29 @@ def _oracle_mask(olb, store, size):
     return m
 
 
-def _record_masks(lb, sink, forced=None, olb=None):
+def _norm_maps(olb, store):
+    """The 16x16 maps null_text.py:41-51 thresholds, BEFORE the threshold: the word-weighted map
+    (alpha words, mean over the 5 stored layers, 3x3 max-pool) and the substruct map (no pool), each
+    normalised by its maximum -- [B, 16, 16] each (sub: None without substruct words).  The nearest
+    upsample to the latent repeats every cell over a 4x4 pixel block, so a mask pixel flips exactly
+    when its cell's value crosses the threshold."""
+    import torch.nn.functional as F
+    maps = store["down_cross"][2:4] + store["up_cross"][:3]
+    maps = torch.cat([t.reshape(olb.B, -1, 1, 16, 16, 77) for t in maps], dim=1)
+    m = F.max_pool2d((maps * olb.alpha).sum(-1).mean(1), (3, 3), (1, 1), padding=(1, 1))
+    m = m / m.amax((2, 3), keepdim=True)
+    sub = None
+    if olb.sub is not None:
+        sub = (maps * olb.sub).sum(-1).mean(1)
+        sub = (sub / sub.amax((2, 3), keepdim=True))[:, 0]
+    return m[:, 0].clone(), sub
+
+
+def _record_masks(lb, sink, forced=None, olb=None, norms=None):
     """Wrap the product LocalBlend's per-step mask (fused latent-step protocol) to keep a copy; with
     olb, also the oracle's mask computed from the PRODUCT's own stored maps of the same step
-    (teacher-forced: same inputs, so only the mask math is compared)."""
+    (teacher-forced: same inputs, so only the mask math is compared) and, in norms, the
+    pre-threshold maps of those stored maps (_norm_maps)."""
     orig = lb.step_mask
 
     def step_mask(store, size, folded=None):
@@ -45,19 +64,24 @@ def _record_masks(lb, sink, forced=None, olb=None):
         sink.append(None if m is None else controllers.as_mask(m).clone())
         if forced is not None:
             forced.append(None if m is None else _oracle_mask(olb, store, size))
+        if norms is not None:
+            norms.append(None if m is None else _norm_maps(olb, store))
         return m
 
     lb.step_mask = step_mask
 
 
-def _record_oracle_masks(olb, sink):
+def _record_oracle_masks(olb, sink, norms=None):
     orig = olb.__call__
 
     class Rec:
         def __call__(self, x_t, store):
             before = olb.counter
             out = orig(x_t, store)
-            sink.append(olb.last_mask.clone() if olb.counter > olb.start_blend and olb.counter != before else None)
+            blended = olb.counter > olb.start_blend and olb.counter != before
+            sink.append(olb.last_mask.clone() if blended else None)
+            if norms is not None:
+                norms.append(_norm_maps(olb, store) if blended else None)
             return out
     return Rec()
 
@@ -72,18 +96,20 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3), unet_dty
         sharpen_attention(model, gain)
     x_T = pl.seed_latent(0)
     from oracle import control as oc
-    pmasks, fmasks = [], []
+    pmasks, fmasks, pnorms, onorms = [], [], [], []
     flb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok, th=th)
     flb.alpha = flb.alpha.to(cuda)
+    if flb.sub is not None:
+        flb.sub = flb.sub.to(cuda)
     with config.compute_mode(compute):
         ctrl = pl.make_replace_controller(prompts, 50, device=cuda, blend_th=th)
-        _record_masks(ctrl.local_blend, pmasks, fmasks, flb)
+        _record_masks(ctrl.local_blend, pmasks, fmasks, flb, pnorms)
         got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=50)
     # the oracle run, recording its LocalBlend mask at every step
     omasks = []
     olb = oc.OracleLocalBlend("null", prompts, pl.BLEND_WORDS, tok, th=th)
     olb.alpha = olb.alpha.to(cuda)
-    octrl = oracle_controller("replace", prompts, tok, 50, cuda, local_blend=_record_oracle_masks(olb, omasks))
+    octrl = oracle_controller("replace", prompts, tok, 50, cuda, local_blend=_record_oracle_masks(olb, omasks, onorms))
     print("product run done", flush=True)
     want = oracle_group(model, prompts, x_T, octrl, 50)
     cos = cosine(got, want)
@@ -117,9 +143,12 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3), unet_dty
     if min(cover) == 1.0:
         assert min(agree) >= 0.999, agree
     else:
+        delta = _explain_flips(pmasks, omasks, agree, pnorms, onorms, th)
+        if len(run_bars) > 2:
+            # every flip sits at a cell whose pre-threshold value the two runs put on either side of
+            # the threshold, and the runs' maps differ by at most run_bars[2] (normalised units)
+            assert delta <= run_bars[2], delta
         assert sum(agree) / n >= run_bars[0] and min(agree) >= run_bars[1], agree
-        if min(agree) < 1.0:
-            _explain_flips(pmasks, omasks, agree)
     if not negatives:
         check_effect(f"configs[1], {str(unet_dtype)[6:]} U-Net + {compute} kernels, gain {gain}", got, want,
                      base_group(model, prompts, x_T, 50), effect_bar)
@@ -145,17 +174,39 @@ def _bench_config_vs_oracle(cuda, tok, gain, effect_bar, th=(0.3, 0.3), unet_dty
         check_negative("LocalBlend off", neg_blend, want, base, effect_bar)
 
 
-def _explain_flips(pmasks, omasks, agree):
-    """For the worst step: how many pixels and 16x16 map cells (4x4 pixel blocks after the nearest
-    upsample) differ between the product's and the oracle's run, per prompt."""
-    i = min(range(len(agree)), key=lambda j: agree[j])
+def _explain_flips(pmasks, omasks, agree, pnorms, onorms, th):   # th = (pool, substruct) thresholds
+    """Where the product's and the oracle's masks differ: per blended step with a difference, the
+    pixels and 16x16 cells that differ, the cells whose pre-threshold value (_norm_maps) the two
+    runs put on opposite sides of the threshold (own word map, or the SOURCE's, which
+    null_text.py:66 ORs into every prompt's mask), their distance from the threshold, and the
+    largest difference between the two runs' normalised maps.  Returns that largest difference over
+    all blended steps."""
     steps = [j for j, m in enumerate(pmasks) if m is not None]
-    s = steps[i]
-    pm, om = pmasks[s] != 0, omasks[s].reshape(pmasks[s].shape)
-    diff = (pm != om)
-    cells = diff[:, 0].reshape(diff.shape[0], 16, 4, 16, 4).any(4).any(2)
-    print(f"  worst step {s}: {int(diff.sum())} pixels = {int(cells.sum())} of {cells.numel()} 16x16 cells differ "
-          f"(per prompt {cells.flatten(1).sum(1).tolist()})", flush=True)
+    worst_delta = 0.0
+    for i, s in enumerate(steps):
+        (pm_, ps_), (om_, os_) = pnorms[s], onorms[s]
+        delta = (pm_ - om_).abs().max().item()
+        if ps_ is not None:
+            delta = max(delta, (ps_ - os_).abs().max().item())
+        worst_delta = max(worst_delta, delta)
+        if agree[i] == 1.0:
+            continue
+        pm, om = pmasks[s] != 0, omasks[s].reshape(pmasks[s].shape)
+        diff = pm != om
+        cells = diff.reshape(diff.shape[0], 16, 4, 16, 4).any(4).any(2)
+        cross = (pm_ > th[0]) != (om_ > th[0])
+        dist = (om_[cross] - th[0]).abs()
+        print(f"  step {s}: {int(diff.sum())} pixels = {int(cells.sum())} cells differ (per prompt "
+              f"{cells.flatten(1).sum(1).tolist()}); cells across the threshold per prompt "
+              f"{cross.flatten(1).sum(1).tolist()} at |oracle - th| {[round(x, 5) for x in dist.tolist()]}; "
+              f"max |product - oracle| of the normalised maps {delta:.2e}", flush=True)
+        # every differing cell is explained: its own map or the source's crosses the threshold
+        explained = cross | cross[:1]
+        if ps_ is not None:
+            explained = explained | ((ps_ > th[1]) != (os_ > th[1]))
+        assert not (cells & ~explained).any()
+    print(f"  largest difference of the two runs' normalised maps over the blended steps: {worst_delta:.2e}")
+    return worst_delta
 
 
 def test_bench_default_config_50_steps(cuda, tok):

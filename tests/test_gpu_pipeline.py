@@ -94,18 +94,17 @@ def test_edit_group_check_mode_tight(cuda, tok):
 
 def test_cross_kv_cache_bit_identical(cuda):
     """The cross-attention K / V projections are computed once per edit group (ptp_utils._cross_kv:
-    the loop's context is one tensor for all steps, ptp_utils.py:158-168): a bf16 edit group with
-    the cache is bit-identical to one that recomputes them at every call, the cached K / V equal a
-    fresh projection of the context, and the cache really served the later steps."""
+    the loop's context is one tensor for all steps, ptp_utils.py:158-168): every cached K / V equals
+    a fresh projection of the context bit for bit, the cache really served the later steps, and a
+    bf16 edit group with the cache is bit-identical to one that recomputes them at every call
+    (after a warm-up group, so both runs meet the same library kernels)."""
     from p2p_amd import ptp_utils as pu
     prompts = pl.north_star_prompts()
     model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
     x_T = pl.seed_latent(5)
     steps = 6
-    calls = []
+    calls, fresh_equal = [], []
     orig = pu._cross_kv
-
-    fresh_equal = []
 
     def counting(module, context, w):
         hit = module.__dict__.get("_p2p_kv")
@@ -114,20 +113,33 @@ def test_cross_kv_cache_bit_identical(cuda):
         if calls[-1]:   # a cached K / V against a fresh projection of the same context
             fresh_equal.append(torch.equal(kv, torch.nn.functional.linear(context, w)))
         return kv
-    pu._cross_kv = counting
-    try:
+
+    def group(cache):
+        pu.CACHE_CROSS_KV = cache
         with config.compute_mode("bf16"):
-            got = pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
-                                    num_steps=steps)
-            pu.CACHE_CROSS_KV = False
-            want = pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
+            return pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
                                      num_steps=steps)
+    # MIOpen's default convolution solvers are not run-to-run reproducible (tools/determinism_probe.py:
+    # two identical U-Net calls differ by up to 2e-2; every hot-path kernel and the U-Net's GEMMs are)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        group(False)                    # warm-up: library kernel selection, workspaces
+        off1 = group(False)
+        pu._cross_kv = counting
+        on = group(True)
+        pu._cross_kv = orig
+        off2 = group(False)
     finally:
         pu._cross_kv = orig
         pu.CACHE_CROSS_KV = True
+        torch.backends.cudnn.deterministic = det
     n_cross = 16
-    assert len(calls) == 2 * steps * n_cross
-    # cache on: the first U-Net call of the group computes, the other steps hit
-    assert calls[:n_cross] == [False] * n_cross and all(calls[n_cross:steps * n_cross]), calls[:steps * n_cross]
+    assert len(calls) == steps * n_cross
+    # the first U-Net call of the group computes, the other steps hit
+    assert calls[:n_cross] == [False] * n_cross and all(calls[n_cross:]), calls
     assert len(fresh_equal) == (steps - 1) * n_cross and all(fresh_equal)
-    assert torch.equal(got, want)
+    print(f"cache off vs off: equal {torch.equal(off1, off2)} max |diff| {(off1 - off2).abs().max().item():.3e}; "
+          f"cache on vs off: equal {torch.equal(on, off1)} max |diff| {(on - off1).abs().max().item():.3e}")
+    assert torch.equal(off1, off2), "the uncached pipeline is not run-to-run reproducible"
+    assert torch.equal(on, off1)
