@@ -229,16 +229,22 @@ def test_bench_config_sharpened_50_steps(cuda, tok):
     _bench_config_vs_oracle(cuda, tok, 4.0, 0.97, th=(0.8, 0.8))
 
 
-@pytest.mark.parametrize("compute, run_bars", [("f32", (0.999, 0.999)), ("bf16", (0.999, 0.995))], ids=["f32", "bf16"])
+@pytest.mark.parametrize("compute, run_bars", [("f32", (0.999, 0.999, 1e-4)), ("bf16", (0.999, 0.96, 1e-3))],
+                         ids=["f32", "bf16"])
 def test_bench_config_f32unet_sharpened_partial_masks(cuda, tok, compute, run_bars):
     """LocalBlend end to end on PARTIAL masks with the U-Net's rounding out of the picture: configs[1]
     (1 source + 3 Replace edits, null_text LocalBlend, 50 DDIM steps) on an f32 U-Net, sharpened
     (every logit x4) with thresholds 0.8, so the masks cover about half the pixels, against the
     oracle's own fp32 run (null_text.py:41-70, main.py:164-167).  North-star bar: the masks agree on
-    >= 99.9 % of the pixels -- at every blended step in the f32 check mode, on average (per-step
-    minimum >= 99.5 %) with the bf16 kernels, whose probabilities sit within 2e-3 of the oracle's
-    and can move a 16x16 map cell that lies that close to its threshold (one cell = 16 of the 4 x
-    64 x 64 pixels = 0.1 %).  Edit-effect bar 0.99 (f32 U-Net)."""
+    >= 99.9 % of the pixels -- at every blended step in the f32 check mode (the two runs' normalised
+    16x16 maps within 1e-4; measured 2e-6), and on average over the 40 blended steps with the bf16
+    kernels.  There the normalised maps differ by at most 1e-3 (measured 1.9-2.3e-4), and a map value
+    that close to the threshold flips a whole block at once: the 3x3 max-pool copies it into 9 cells
+    (4x4 pixels each after the upsample), and null_text.py:66 ORs the SOURCE's mask into every
+    prompt's, so one source value 4e-5 from the threshold moved 352 of 16384 pixels (97.9 %) in a
+    logged run (profiles/r06/localblend_f32unet.log); the per-step bar is therefore 96 % (one such
+    block in all four prompts: 4 x 9 x 16 pixels = 3.5 %), and every differing cell must be explained
+    by a map value across the threshold (_explain_flips).  Edit-effect bar 0.99 (f32 U-Net)."""
     _bench_config_vs_oracle(cuda, tok, 4.0, EFFECT_BAR, th=(0.8, 0.8), unet_dtype=torch.float32, compute=compute,
                             run_bars=run_bars, negatives=False)
 
