@@ -110,28 +110,40 @@ NOMINAL_SCLK_MHZ = 2400.0       # the clock the dense peak assumes: 256 CU x 4 S
 
 class ClockProbe:
     """The shader clock the chip holds during the timed run (p2p_clock_probe, include/p2p_hip.h):
-    8 one-wave workgroups (one per XCD) each count shader cycles against the constant 100 MHz
-    counter over `ticks` (10 us).  Sampled at the start and the end of the timed region and right
-    after every `every`-th dominant-kernel launch (after its end event, so it sits in no attention
-    launch's timing window): DVFS moves the clock on a millisecond scale, so a probe queued right
-    behind the G1/G7 kernel reads the clock the chip was holding for it.  Each sample = the median
-    over the 8 workgroups."""
+    8 one-wave workgroups (consecutive workgroups go to the 8 XCDs) each count shader cycles
+    against the constant 100 MHz counter.  Two kinds of sample, each the median over the 8:
+    * "during": every `every`-th dominant-kernel (G1/G7) launch, a probe of `ticks_during` (100 us,
+      about half the kernel) on a second stream released together with the kernel, so it runs
+      on 8 CUs while G1/G7 holds the other 248: the clock the chip holds under that kernel's load.
+      Those launches lose 8 CUs (512 workgroups then need a third round: +30 %), so they leave
+      every average (dominant kernel and all-attention totals) and are reported on their own;
+    * "start" / "end": a 10 us probe on the launch stream at the start / end of the timed region
+      (the chip at rest between launches)."""
 
-    def __init__(self, device, max_samples=512, every=25, ticks=1000):
+    def __init__(self, device, max_samples=512, every=25, ticks=1000, ticks_during=10000):
         from p2p_amd import _hip
         self._hip = _hip
         self.buf = torch.zeros(max_samples, 8, 2, dtype=torch.int64, device=device)
-        self.tags, self.every, self.ticks, self.n_dominant = [], every, ticks, 0
+        self.side = torch.cuda.Stream(device)
+        self.tags, self.every, self.ticks, self.ticks_during, self.n_dominant = [], every, ticks, ticks_during, 0
 
-    def sample(self, tag):
+    def sample(self, tag, ticks=None):
         if len(self.tags) < self.buf.shape[0]:
-            self._hip.clock_probe(self.buf[len(self.tags)], self.ticks)
+            self._hip.clock_probe(self.buf[len(self.tags)], ticks or self.ticks)
             self.tags.append(tag)
+            return True
+        return False
 
-    def after_dominant(self):
+    def during_dominant(self) -> bool:
+        """Called right before a dominant-kernel launch: True when this launch is probed."""
         self.n_dominant += 1
-        if self.n_dominant % self.every == 0:
-            self.sample("pipeline")
+        if self.n_dominant % self.every or len(self.tags) >= self.buf.shape[0]:
+            return False
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)           # released when the kernel before G1/G7 ends
+        with torch.cuda.stream(self.side):
+            self.sample("during", self.ticks_during)
+        return True
 
     def summary(self):
         torch.cuda.synchronize()
@@ -140,11 +152,11 @@ class ClockProbe:
             return None
         b = self.buf[:n].double().cpu()
         mhz = (b[..., 0] / b[..., 1].clamp(min=1) * 100.0).median(dim=1).values.tolist()
-        pipe = sorted(m for m, t in zip(mhz, self.tags) if t == "pipeline")
-        edge = {t: round(m, 1) for m, t in zip(mhz, self.tags) if t != "pipeline"}
-        return {"sclk_mhz": (pipe[len(pipe) // 2] if pipe else sorted(mhz)[n // 2]),
-                "pipeline_samples": len(pipe), "pipeline_min_mhz": pipe[0] if pipe else None,
-                "pipeline_max_mhz": pipe[-1] if pipe else None, **{f"{k}_mhz": v for k, v in edge.items()}}
+        during = sorted(m for m, t in zip(mhz, self.tags) if t == "during")
+        edge = {t: round(m, 1) for m, t in zip(mhz, self.tags) if t != "during"}
+        return {"sclk_mhz": (during[len(during) // 2] if during else sorted(mhz)[n // 2]),
+                "during_samples": len(during), "during_min_mhz": during[0] if during else None,
+                "during_max_mhz": during[-1] if during else None, **{f"{k}_mhz": v for k, v in edge.items()}}
 
 
 class LaunchTimer:
@@ -171,7 +183,7 @@ class LaunchTimer:
         self.batch = 0
         self.batch_marks = []    # one event at the end of each timed batch
         self.cross_group_kernel = {}   # geometry name -> True when the group cross kernel ran
-        self.clock = None              # a ClockProbe sampled behind the dominant kernel
+        self.clock = None              # a ClockProbe sampled during the dominant kernel
 
     @staticmethod
     def _bytes(kind, t, info):
@@ -197,7 +209,11 @@ class LaunchTimer:
         if not self.enabled:
             return
         info = info or {"stored": 0, "accumulate": False}
-        self._open(self._names(kind, t, info))
+        names = self._names(kind, t, info)
+        if self.clock is not None and any(n == "dominant" for n, _ in names) and self.clock.during_dominant():
+            # a probed launch runs on 248 CUs (a third round of workgroups): it leaves every average
+            names = [("dominant_probed", w) for n, w in names if n == "dominant"]
+        self._open(names)
         if kind == "cross" and "n_groups" in info:
             self.cross_group_kernel[f"attn:cross:P{t.n_query}:d{t.head_dim}"] = bool(info.get("group_kernel"))
 
@@ -224,8 +240,6 @@ class LaunchTimer:
             for name, work in names:
                 self.rec.setdefault(name, []).append((start, ev, work, self.batch))
             self._pending = None
-            if self.clock is not None and any(n == "dominant" for n, _ in names):
-                self.clock.after_dominant()
 
     def before_aux(self, name, nbytes):
         """The LocalBlend mask and latent-step launches (HBM-type helpers), with their bytes."""
@@ -364,10 +378,11 @@ def _clock_fields(clk, frac):
         return {"sclk_mhz": None, "frac_at_measured_clock": None}
     return {"sclk_mhz": clk["sclk_mhz"], "nominal_sclk_mhz": NOMINAL_SCLK_MHZ,
             "frac_at_measured_clock": frac * NOMINAL_SCLK_MHZ / clk["sclk_mhz"] if frac else None,
-            "clock_probe": {**clk, "rule": "p2p_clock_probe: 8 one-wave workgroups count shader cycles over 10 us "
-                                           "of the 100 MHz counter; sampled after every 25th G1/G7 launch and at "
-                                           "the start / end of the timed region; sclk = median of the in-pipeline "
-                                           "samples"}}
+            "clock_probe": {**clk, "rule": "p2p_clock_probe: 8 one-wave workgroups count shader cycles against the "
+                                           "100 MHz counter; 'during' = a 100 us probe on a second stream running "
+                                           "beside every 25th G1/G7 launch (those launches leave the average); "
+                                           "start / end = 10 us probes at the edges of the timed region; sclk = "
+                                           "median of the 'during' samples"}}
 
 
 def pmc_traffic():
@@ -561,6 +576,8 @@ def main():
                     "kernel": f"self40_kernel G1/G7, F16 form (P=K=4096, d=40, N={8 * G}, H=8; 8 waves x 2 x 32 queries, "
                               f"256-key tiles, software-pipelined 32x32 blocks)",
                     "avg_launch_ms": avg_ms, "launches": n_launch,
+                    "probed_launches": {"avg_launch_ms": timer.summary("dominant_probed")[0],
+                                        "launches": timer.summary("dominant_probed")[2]},
                     "flop_per_launch": flops,
                     **_clock_fields(clock.summary(), (achieved / peak) if achieved else None),
                     "timing": {"ext": "HIP events bound to each launch's kernels (hipExtLaunchKernel start / stop "
