@@ -39,7 +39,12 @@ enum {
    * step inside cross_replace_steps, main.py:189), so P_e' = R and the edit entries' own Q K^T
    * softmax, Q and K are not needed -- the bf16 dense kernels then load only their V.  The
    * kernel re-derives A from the program and falls back to the full edit if the hint is wrong. */
-  P2P_GROUP_F_R_ONLY = 2
+  P2P_GROUP_F_R_ONLY = 2,
+  /* p2p_group.flags (ABI 15), a caller guarantee, also for groups without a program: every entry
+   * of the group has the SAME K and V values as its first entry (the uncond prompts "" of a group,
+   * ptp_utils.py:150-156, whose context rows are equal).  The group kernel then stages them once
+   * per workgroup instead of per entry; results are bit-identical when the guarantee holds. */
+  P2P_GROUP_F_SHARED_KV = 4
 };
 
 enum { P2P_DTYPE_F32 = 0, P2P_DTYPE_BF16 = 1 };

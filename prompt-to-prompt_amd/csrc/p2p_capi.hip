@@ -155,7 +155,7 @@ int p2p_cross_attn_fwd(const p2p_attn_tensors* t, const p2p_group* groups, int32
                                (int64_t)G.n_edits * P2P_PROGRAM_REC_BYTES
                          : nullptr;
     a.grp_alpha[g] = G.alpha;
-    a.grp_flags[g] = G.program ? G.flags : 0;
+    a.grp_flags[g] = G.program ? G.flags : (G.flags & P2P_GROUP_F_SHARED_KV);
     a.grp_bsum[g] = G.blend_sums;
     a.grp_balpha[g] = G.blend_alpha;
     a.grp_bsub[g] = G.blend_sub;

@@ -135,6 +135,17 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   const bool prow = p < P;
   float* const slab = reinterpret_cast<float*>(cross_dyn) + wave * 32 * K;
   const bool blend_on = STORE && a.grp_bsum[gi] != nullptr;
+  // p2p_group.flags hints (include/p2p_hip.h), workgroup-uniform:
+  //  * R_ONLY: every edit's blend reads only R = P0 M_e this call, so an edit entry needs its V
+  //    but not its K and Q -- they are not loaded (a wrong hint reloads them after the entry's
+  //    coefficients show it, below);
+  //  * SHARED_KV: every entry of the group has the first entry's K and V (the uncond prompts ""):
+  //    they are staged once, and a plain group then rewrites no LDS between its entries, so the
+  //    barrier pair between entries goes too
+  const int gflags = a.grp_flags[gi];
+  const bool hint_r = EDIT && edits && (gflags & P2P_GROUP_F_R_ONLY) != 0;
+  const bool shared_kv = (gflags & P2P_GROUP_F_SHARED_KV) != 0;
+  const bool no_sync = shared_kv && !edits && !blend_on;
 
   // ---- padding the MFMAs read and the staging never writes (written once; the staging writes
   // columns < D): K columns D..DK (met by Q's zero columns)
@@ -166,27 +177,55 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   short8_t qf[NKT];
   // Range-checked buffer loads throughout (zeros past the range): no per-chunk branches, so
   // the whole entry issues as one straight run of loads
-  auto load_entry = [&](int b) __attribute__((always_inline)) {
-    const int e = first + b;
+  // the entry's K (own softmax), V and Q rows; rows >= K read as zeros (K rows are masked; V rows
+  // past K must be zero), Q rows >= P as zeros (columns >= D are zeroed when consumed)
+  auto load_k = [&](int e) __attribute__((always_inline)) {
     const char* kp = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.k) + (int64_t)e * a.bsk + h * D);
-    const char* vp = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.v) + (int64_t)e * a.bsv + h * D);
-    // rows >= K read as zeros (K rows are masked; V rows past K must be zero)
     const __amdgpu_buffer_rsrc_t rk = make_rsrc(kp, ((int64_t)(K - 1) * a.ldk + D) * 2);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(vp, ((int64_t)(K - 1) * a.ldv + D) * 2);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int cidx = tid + i * NT;
       const int row = cidx / CPR;
       const int ch = cidx - row * CPR;
       kreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rk, (row * (int)a.ldk + ch * 8) * 2, 0, 0));
-      vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (row * (int)a.ldv + ch * 8) * 2, 0, 0));
     }
-    // Q rows >= P read as zeros; columns >= D are zeroed when the fragments are consumed
+  };
+  auto load_q = [&](int e) __attribute__((always_inline)) {
     const char* qp = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.q) + (int64_t)e * a.bsq + h * D);
     const __amdgpu_buffer_rsrc_t rq = make_rsrc(qp, ((int64_t)(P - 1) * a.ldq + D) * 2);
 #pragma unroll
     for (int t = 0; t < NKT; ++t)
       qf[t] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rq, (p * (int)a.ldq + 16 * t + 8 * hh) * 2, 0, 0));
+  };
+  auto write_k = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cidx = tid + i * NT;
+      const int row = cidx / CPR;
+      const int ch = cidx - row * CPR;
+      if ((KR * CPR) % NT == 0 || cidx < KR * CPR) *reinterpret_cast<short8_t*>(Ks + row * KS + ch * 8) = kreg[i];
+    }
+  };
+  // which of the entry's rows are staged (workgroup-uniform): K only where the entry's own
+  // softmax can run, V unless the group shares the first entry's, Q only with its own softmax
+  auto stage_k = [&](int b) { return !(b > 0 && (shared_kv || hint_r)); };
+  auto stage_v = [&](int b) { return !(b > 0 && shared_kv); };
+  auto stage_q = [&](int b) { return !(b > 0 && hint_r); };
+  auto load_entry = [&](int b) __attribute__((always_inline)) {
+    const int e = first + b;
+    if (stage_k(b)) load_k(e);
+    if (stage_v(b)) {
+      const char* vp = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.v) + (int64_t)e * a.bsv + h * D);
+      const __amdgpu_buffer_rsrc_t rv = make_rsrc(vp, ((int64_t)(K - 1) * a.ldv + D) * 2);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int cidx = tid + i * NT;
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        vreg[i] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rv, (row * (int)a.ldv + ch * 8) * 2, 0, 0));
+      }
+    }
+    if (stage_q(b)) load_q(e);
     if constexpr (EDIT) {
       if (edits && b > 0) {
         // mapper rows >= K are zero in the program and never staged
@@ -220,14 +259,14 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     // HERE: otherwise the loop header merges Q as pending and the next Q K^T waits with a vmcnt
     // that also drains the following entry's prefetch
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    if (stage_k(b)) write_k();   // rows past K are the zeros the loads returned
+    if (stage_v(b)) {
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int cidx = tid + i * NT;
-      const int row = cidx / CPR;
-      const int ch = cidx - row * CPR;
-      if ((KR * CPR) % NT == 0 || cidx < KR * CPR) {   // rows past K are the zeros the loads returned
-        *reinterpret_cast<short8_t*>(Ks + row * KS + ch * 8) = kreg[i];
-        *reinterpret_cast<short8_t*>(Vs + row * VS + ch * 8) = vreg[i];
+      for (int i = 0; i < NCH; ++i) {
+        const int cidx = tid + i * NT;
+        const int row = cidx / CPR;
+        const int ch = cidx - row * CPR;
+        if ((KR * CPR) % NT == 0 || cidx < KR * CPR) *reinterpret_cast<short8_t*>(Vs + row * VS + ch * 8) = vreg[i];
       }
     }
     if constexpr (EDIT) {
@@ -526,7 +565,11 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
         }
     }
     P2P_GROUP_STAMP(5 + 5 * b)
-    if (more) {
+    if (more && no_sync) {
+      // shared K / V, no program, no blend table: nothing in LDS changes for the next entry; its Q
+      // rows retire here (as in write_entry), not in the next entry's first Q K^T
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    } else if (more) {
       __syncthreads();   // every wave is done with this entry's K, V, mapper and coefficients
       write_entry(b + 1);
       __syncthreads();
@@ -538,6 +581,15 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
           const bool a0 = c0 < K && coef[c0] != 0.f, a1 = c1 < K && coef[c1] != 0.f;
           const bool b0 = c0 < K && coef[KR + c0] != 0.f, b1 = c1 < K && coef[KR + c1] != 0.f;
           next_flags = (__any(a0 || a1) ? 1 : 0) | (__any(b0 || b1) ? 2 : 0);
+          if (hint_r && (next_flags & 1)) {
+            // a wrong R_ONLY hint (some A != 0): the next edit runs its own softmax after all, so
+            // its K and Q rows come now (every wave reads the same coefficients: uniform branch)
+            load_k(first + b + 1);
+            load_q(first + b + 1);
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+            write_k();
+            __syncthreads();
+          }
         }
       }
     }

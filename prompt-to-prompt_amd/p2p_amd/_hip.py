@@ -34,6 +34,7 @@ PROGRAM_COLS = 128
 PROGRAM_TMAX = 8
 ABI_VERSION = 15
 GROUP_F_R_ONLY = 2      # p2p_group.flags: every edit's blend coefficient A is 0 this call (P' = R)
+GROUP_F_SHARED_KV = 4   # p2p_group.flags: every entry of the group has the first entry's K and V
 
 
 class HipError(RuntimeError):
@@ -266,6 +267,18 @@ def cross_group_dispatch(t: AttnTensors, groups) -> bool:
     return len(groups) * t.n_heads * ((t.n_query + 127) // 128) >= 512
 
 
+SHARED_KV_HINTS = os.environ.get("P2P_SHARED_KV", "1") != "0"   # (A/B switch: 0 = never hint)
+
+
+def shared_kv_hint(k, v, first: int, count: int) -> int:
+    """GROUP_F_SHARED_KV when the K and V rows first .. first + count - 1 are bit-identical, as
+    recorded on the projection views by ptp_utils._project (kv_row_classes); else 0."""
+    rows = getattr(k, "_p2p_rows", None)
+    if not SHARED_KV_HINTS or count < 2 or rows is None or getattr(v, "_p2p_rows", None) is not rows or len(rows) != k.shape[0]:
+        return 0
+    return GROUP_F_SHARED_KV if all(r == rows[first] for r in rows[first:first + count]) else 0
+
+
 def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, store_slot=None,
                accumulate=False):
     """groups: list of (first, count, program_tensor|None, alpha_tensor|None[, blend[, hints]]) with
@@ -281,7 +294,7 @@ def cross_attn(q, k, v, o, heads, scale, groups, compute="bf16", store=None, sto
         G[i].first, G[i].count = int(first), int(count)
         G[i].program = prog.data_ptr() if prog is not None else None
         G[i].alpha = alpha.data_ptr() if alpha is not None else None
-        G[i].flags = (int(getattr(prog, "p2p_flags", 0)) | hints) if prog is not None else 0
+        G[i].flags = (int(getattr(prog, "p2p_flags", 0)) | hints) if prog is not None else (hints & GROUP_F_SHARED_KV)
         G[i].n_edits = int(getattr(prog, "p2p_n_edits", 0)) if prog is not None else 0
         if blend is not None:
             sums, balpha, bsub, col, lh = blend

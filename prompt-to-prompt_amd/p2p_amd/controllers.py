@@ -574,7 +574,9 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
         out = torch.empty_like(q)
         if is_cross:
             blend = self._blend_fold(self._last_store_key, P, K, heads, q.device) if store is not None else None
-            groups = ([(0, n0, None, None)] if n0 else []) + [(n0, n_cond, prog, alpha.contiguous(), blend, hints)]
+            # the uncond rows ("" prompts) share their K / V: staged once per workgroup (SHARED_KV)
+            groups = (([(0, n0, None, None, None, _hip.shared_kv_hint(k, v, 0, n0))] if n0 else [])
+                      + [(n0, n_cond, prog, alpha.contiguous(), blend, hints)])
             _hip.cross_attn(q, k, v, out, heads, scale, groups, compute=config.COMPUTE, store=store,
                             store_slot=slots, accumulate=acc)
         else:
@@ -792,7 +794,7 @@ class GroupBatch(AttentionControl):
             slots = [-1] * GB + [(n - GB) * heads for n in range(GB, N)]
         out = torch.empty_like(q)
         if is_cross and K <= _hip.MAX_KEYS_CROSS:
-            groups = [(0, GB, None, None)]
+            groups = [(0, GB, None, None, None, _hip.shared_kv_hint(k, v, 0, GB))]
             for g, m in enumerate(self.members):
                 first = GB + g * B
                 if isinstance(m, AttentionControlEdit):

@@ -222,13 +222,27 @@ def _cross_kv(module, context, w):
     import weakref
     if (not CACHE_CROSS_KV or context.is_inference() or context.requires_grad
             or (context.is_cuda and torch.cuda.is_current_stream_capturing())):
-        return torch.nn.functional.linear(context, w)
+        return torch.nn.functional.linear(context, w), None
     hit = module.__dict__.get("_p2p_kv")
     if hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w:
-        return hit[3]
+        return hit[3], hit[4]
     kv = torch.nn.functional.linear(context, w)
-    module.__dict__["_p2p_kv"] = (weakref.ref(context), context._version, w, kv)
-    return kv
+    rows = kv_row_classes(kv)
+    module.__dict__["_p2p_kv"] = (weakref.ref(context), context._version, w, kv, rows)
+    return kv, rows
+
+
+def kv_row_classes(kv):
+    """For each batch row of a cross-attention's K / V projection, the first row of its run of
+    bit-identical rows (rows n and n + 1 compared exactly) -- e.g. the uncond prompts "" of a group
+    (ptp_utils.py:150-156) give equal context rows, hence equal K and V.  Computed once per cached
+    projection (one device -> host read); the controllers turn it into p2p_group's SHARED_KV."""
+    flat = kv.reshape(kv.shape[0], -1)
+    same = (flat[1:] == flat[:-1]).all(dim=1).tolist()
+    rows = [0]
+    for i, eq in enumerate(same):
+        rows.append(rows[-1] if eq else i + 1)
+    return tuple(rows)
 
 
 def _project(module, x, context, is_cross):
@@ -242,9 +256,12 @@ def _project(module, x, context, is_cross):
         if is_cross:
             w = _stacked_weight(module, ("to_k", "to_v"))
             if w is not None:
-                kv = _cross_kv(module, src, w)
+                kv, rows = _cross_kv(module, src, w)
                 C = kv.shape[-1] // 2
-                return module.to_q(x), kv[..., :C], kv[..., C:]
+                k, v = kv[..., :C], kv[..., C:]
+                if rows is not None:
+                    k._p2p_rows = v._p2p_rows = rows   # (read by the controllers' group hints)
+                return module.to_q(x), k, v
         else:
             w = _stacked_weight(module, ("to_q", "to_k", "to_v"))
             if w is not None:

@@ -456,3 +456,48 @@ def test_cross_r_only_hint(cuda, geom):
     p = ref_probs(q, k, H, scale)
     R = torch.einsum("hpw,bwn->bhpn", p[BG], _edit_mapper(B, K).to(cuda))
     assert (store[H:B * H] - 2 * R.reshape((B - 1) * H, P, K)).abs().max().item() < 2 * 2e-3
+
+
+@pytest.mark.parametrize("geom", [(4096, 40, 1, "group"), (4096, 40, 2, "group"), (4000, 40, 1, "group"),
+                                  (1024, 80, 1, "entry"), (256, 160, 8, "entry")],
+                         ids=lambda g: "P{}_d{}_g{}_{}".format(*g))
+def test_cross_shared_kv_hint(cuda, geom):
+    """p2p_group.flags GROUP_F_SHARED_KV (ABI 15): the caller's guarantee that every entry of a group
+    has the first entry's K and V (the uncond prompts ""); the group kernel stages them once and a
+    plain group drops its barriers between entries.  With equal uncond rows the hinted launch is
+    bit-identical to the unhinted one -- plain steps, R_ONLY edit steps, and one uncond group of
+    every prompt group's rows (GroupBatch) -- and the per-entry kernel ignores the flag."""
+    from p2p_amd import programs
+    P, d, n_groups, kernel = geom
+    B, H, K = 4, 8, 77
+    BG = B * n_groups
+    N = 2 * BG
+    q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=6.0, seed=91 + P)
+    k[1:BG] = k[0]
+    v[1:BG] = v[0]
+    scale = d ** -0.5
+    prog = programs.replace_program(_edit_mapper(B, K)).to_device(cuda)
+    ones = torch.ones(B - 1, K, device=cuda)
+
+    def run(uncond, edits, shared):
+        o = torch.empty_like(q)
+        hint = _hip.GROUP_F_SHARED_KV if shared else 0
+        groups = [(f, c, None, None, None, hint) for f, c in uncond]
+        groups += [(BG + g * B, B, prog, ones, None, _hip.GROUP_F_R_ONLY) if edits else (BG + g * B, B, None, None)
+                   for g in range(n_groups)]
+        _hip.cross_attn(q, k, v, o, H, scale, groups)
+        return o, groups
+
+    per_group = [(g * B, B) for g in range(n_groups)]
+    for uncond in (per_group, [(0, BG)]):
+        for edits in (False, True):
+            want, groups = run(uncond, edits, False)
+            got, _ = run(uncond, edits, True)
+            t = _hip.make_tensors(q, k, v, want, H, scale, "bf16")
+            if uncond is per_group:
+                assert _hip.cross_group_dispatch(t, groups) == (kernel == "group")
+            assert torch.equal(got, want), (got.float() - want.float()).abs().max().item()
+    # and it is attention: the uncond rows against fp32 torch
+    o, _ = run(per_group, True, True)
+    p = ref_probs(q, k, H, scale)
+    assert (o[:BG].float() - ref_out(p, v, H)[:BG]).abs().max().item() < o_tol(v, "bf16")

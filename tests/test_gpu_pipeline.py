@@ -109,10 +109,10 @@ def test_cross_kv_cache_bit_identical(cuda):
     def counting(module, context, w):
         hit = module.__dict__.get("_p2p_kv")
         calls.append(hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w)
-        kv = orig(module, context, w)
+        kv, rows = orig(module, context, w)
         if calls[-1]:   # a cached K / V against a fresh projection of the same context
             fresh_equal.append(torch.equal(kv, torch.nn.functional.linear(context, w)))
-        return kv
+        return kv, rows
 
     def group(cache):
         pu.CACHE_CROSS_KV = cache

@@ -268,12 +268,13 @@ def test_cross_kv_cache_rules():
         return orig(x, weight, bias)
     torch.nn.functional.linear = counting
     try:
-        a = pu._cross_kv(m, ctx, w)
-        b = pu._cross_kv(m, ctx, w)
-        assert b is a and len(calls) == 1
+        a, rows = pu._cross_kv(m, ctx, w)
+        b, rows2 = pu._cross_kv(m, ctx, w)
+        assert b is a and rows2 is rows and len(calls) == 1
+        assert rows == (0, 1)
         assert torch.equal(a, orig(ctx, w))
         ctx.mul_(2.0)                              # in place: the version counter moves
-        c = pu._cross_kv(m, ctx, w)
+        c, _ = pu._cross_kv(m, ctx, w)
         assert len(calls) == 2 and torch.equal(c, orig(ctx, w))
         other = ctx.clone()                        # equal contents, another tensor
         pu._cross_kv(m, other, w)
@@ -293,3 +294,25 @@ def test_cross_kv_cache_rules():
     finally:
         torch.nn.functional.linear = orig
         pu.CACHE_CROSS_KV = True
+
+
+def test_kv_row_classes_and_shared_kv_hint():
+    """ptp_utils.kv_row_classes marks runs of bit-identical K / V rows (the uncond prompts "" of a
+    group); _hip.shared_kv_hint turns a group whose rows all share one class into SHARED_KV."""
+    from p2p_amd import _hip
+    from p2p_amd import ptp_utils as pu
+    g = torch.Generator().manual_seed(1)
+    a, b = torch.randn(77, 16, generator=g), torch.randn(77, 16, generator=g)
+    kv = torch.stack([a, a, a, a, b, a, b, b])
+    rows = pu.kv_row_classes(kv)
+    assert rows == (0, 0, 0, 0, 4, 5, 6, 6)
+    k, v = kv[..., :8], kv[..., 8:]
+    assert _hip.shared_kv_hint(k, v, 0, 4) == 0            # no row classes on the views yet
+    k._p2p_rows = v._p2p_rows = rows
+    assert _hip.shared_kv_hint(k, v, 0, 4) == _hip.GROUP_F_SHARED_KV
+    assert _hip.shared_kv_hint(k, v, 6, 2) == _hip.GROUP_F_SHARED_KV
+    assert _hip.shared_kv_hint(k, v, 4, 4) == 0             # rows 4, 5 differ
+    assert _hip.shared_kv_hint(k, v, 0, 1) == 0             # one entry: nothing to share
+    kv2 = kv.clone()
+    kv2[2, 5, 3] += 1.0                                      # one element differs: not shared
+    assert pu.kv_row_classes(kv2)[:4] == (0, 0, 2, 3)
