@@ -146,6 +146,17 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   const bool hint_r = EDIT && edits && (gflags & P2P_GROUP_F_R_ONLY) != 0;
   const bool shared_kv = (gflags & P2P_GROUP_F_SHARED_KV) != 0;
   const bool no_sync = shared_kv && !edits && !blend_on;
+  // The mapper tile M_e (source word x target word, f16) is built in LDS from the program's term
+  // planes (include/p2p_hip.h: plane t of column w = (source row, value), (0, 0) past the column's
+  // last term) instead of copied from its 18 KiB dense image: the tile is zeroed once, then per
+  // edit the thread of column w clears the previous edit's terms of its column and writes its own
+  // -- the same f16 values at the same places as the dense image (a dense program's values are
+  // exact in f16; a column's terms have distinct rows).  Two planes are prefetched with the entry;
+  // a program whose columns gather more than two source words (tmax > 2, header int 2) copies the
+  // dense image instead, loaded when it is written.
+  const int tmax = edits ? __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(prog)[2]) : 0;
+  const bool terms2 = tmax <= 2;
+  int2 tnew[2] = {{0, 0}, {0, 0}}, tprev[2] = {{0, 0}, {0, 0}};
 
   // ---- padding the MFMAs read and the staging never writes (written once; the staging writes
   // columns < D): K columns D..DK (met by Q's zero columns)
@@ -166,13 +177,15 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   // the K key rows and 0 past them, so O^T row D is the row sum of the bf16 weights P V used: the
   // plain entries take that sum instead of an f32 sum and a normalised P (the staging never
   // writes column D, so this holds for every entry)
+  if constexpr (EDIT)
+    if (edits)
+      for (int i = tid; i < MD * MD / 8; i += NT) reinterpret_cast<short8_t*>(Ms)[i] = short8_t{};
   constexpr bool kOnesCol = DV > D;   // (d = 160, experiments builds only: no padding column)
   if constexpr (kOnesCol)
     for (int r = tid; r < KR; r += NT) Vs[r * VS + D] = r < K ? (uint16_t)0x3F80 : (uint16_t)0;
 
   // ---- the pipelined entry loads: K / V chunks, mapper chunks, coefficients, blend weights, Q
   short8_t kreg[NCH], vreg[NCH];
-  short8_t mreg[EDIT ? NMC : 1];
   float creg[3] = {0.f, 0.f, 0.f}, breg[2] = {0.f, 0.f};   // raw loads, used at LDS-write time
   short8_t qf[NKT];
   // Range-checked buffer loads throughout (zeros past the range): no per-chunk branches, so
@@ -228,15 +241,18 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     if (stage_q(b)) load_q(e);
     if constexpr (EDIT) {
       if (edits && b > 0) {
-        // mapper rows >= K are zero in the program and never staged
-        const __amdgpu_buffer_rsrc_t rm = make_rsrc(static_cast<const uint16_t*>(a.grp_dense[gi]) + (int64_t)(b - 1) * MD * MD,
-                                                    (int64_t)K * MCPR * 16);
+        const char* ce = prog + P2P_PROGRAM_HEADER_BYTES + (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES;
+        // term planes 0 and 1 of column tid (columns >= K hold (0, 0); threads past the tile's
+        // columns read nothing)
+        const __amdgpu_buffer_rsrc_t rt = make_rsrc(ce + 2 * 4 * P2P_PROGRAM_COLS, terms2 ? 2 * 8 * P2P_PROGRAM_COLS : 0);
+        const int toff = tid < MD ? tid * 8 : 1 << 30;
 #pragma unroll
-        for (int j = 0; j < NMC; ++j)
-          mreg[j] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rm, (tid + j * NT) * 16, 0, 0));
+        for (int t = 0; t < 2; ++t) {
+          const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rt, toff + t * 8 * P2P_PROGRAM_COLS, 0, 0);
+          tnew[t] = int2{(int)v2[0], (int)v2[1]};
+        }
         // the column's alpha, c_rep and post (one column per thread, zeros past K); the
         // coefficients are formed at LDS-write time, so nothing here waits for these loads
-        const char* ce = prog + P2P_PROGRAM_HEADER_BYTES + (int64_t)(b - 1) * P2P_PROGRAM_REC_BYTES;
         const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.grp_alpha[gi] + (int64_t)(b - 1) * K, (int64_t)K * 4);
         const __amdgpu_buffer_rsrc_t rc = make_rsrc(ce, (int64_t)K * 4);
         const __amdgpu_buffer_rsrc_t rp = make_rsrc(ce + 4 * P2P_PROGRAM_COLS, (int64_t)K * 4);
@@ -271,10 +287,28 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
     }
     if constexpr (EDIT) {
       if (edits && b > 0) {
+        if (terms2) {
+          if (tid < MD) {
 #pragma unroll
-        for (int j = 0; j < NMC; ++j) {
-          const int i = tid + j * NT;
-          if ((KR * MCPR) % NT == 0 || i < KR * MCPR) reinterpret_cast<short8_t*>(Ms)[i] = mreg[j];
+            for (int t = 0; t < 2; ++t)   // the previous edit's terms of this column
+              if (tprev[t].y != 0 && (unsigned)tprev[t].x < (unsigned)MD) Ms[tprev[t].x * MD + tid] = 0;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+              if (tnew[t].y != 0 && (unsigned)tnew[t].x < (unsigned)MD)
+                Ms[tnew[t].x * MD + tid] = __builtin_bit_cast(uint16_t, (_Float16)__int_as_float(tnew[t].y));
+            tprev[0] = tnew[0];
+            tprev[1] = tnew[1];
+          }
+        } else {
+          // tmax > 2: the dense image (mapper rows >= K are zero in the program and never staged)
+          const __amdgpu_buffer_rsrc_t rm = make_rsrc(static_cast<const uint16_t*>(a.grp_dense[gi]) + (int64_t)(b - 1) * MD * MD,
+                                                      (int64_t)K * MCPR * 16);
+#pragma unroll
+          for (int j = 0; j < NMC; ++j) {
+            const int i = tid + j * NT;
+            const short8_t mc = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rm, i * 16, 0, 0));
+            if ((KR * MCPR) % NT == 0 || i < KR * MCPR) reinterpret_cast<short8_t*>(Ms)[i] = mc;
+          }
         }
         // P' = alpha post (c_rep P_b + R) + (1 - alpha) P_b = P_b A + R B; columns >= K: A = 1, B = 0
         if (tid < KR) {

@@ -350,7 +350,13 @@ def test_cross_group_kernel_bf16(cuda, case):
     q, k, v = make_qkv(N, P, K, H, d, torch.bfloat16, qscale=6.0, seed=31 + P)
     scale = d ** -0.5
     mappers = [_edit_mapper(B, K) if g % 2 == 0 else _edit_mapper(B, K).flip(0) for g in range(n_groups)]
+    if n_groups > 1:
+        # group 1: a target word gathering three source words (tmax 3): the group kernel copies that
+        # program's dense mapper image instead of building the tile from two term planes
+        mappers[1][0, :, 5] = 0.0
+        mappers[1][0, 5, 5], mappers[1][0, 6, 5], mappers[1][0, 9, 5] = 0.25, 0.25, 0.5
     progs = [programs.replace_program(m).to_device(cuda) for m in mappers]
+    assert n_groups == 1 or programs.replace_program(mappers[1]).tmax == 3
     alpha = torch.ones(B - 1, K, device=cuda)      # edit 0: alpha 1 everywhere (R only)
     alpha[1] = 0.0                                   # edit 1: alpha 0 everywhere (own P only)
     alpha[2, 10:20] = 0.0                            # edit 2: both halves

@@ -316,3 +316,44 @@ def test_kv_row_classes_and_shared_kv_hint():
     kv2 = kv.clone()
     kv2[2, 5, 3] += 1.0                                      # one element differs: not shared
     assert pu.kv_row_classes(kv2)[:4] == (0, 0, 2, 3)
+
+
+def _tile_from_terms(blob, e):
+    """The group cross kernel's mapper tile of edit e (p2p_cross.hip): zeros, then per column w the
+    value of each of the first two term planes written at (row, w) where the value is non-zero."""
+    hdr = blob[:32].view(np.int32)
+    rec = blob[programs.HEADER_BYTES + e * programs.REC_BYTES:programs.HEADER_BYTES + (e + 1) * programs.REC_BYTES]
+    planes = rec[8 * COLS:].view(np.int32).reshape(programs.PROGRAM_TMAX, COLS, 2)
+    tile = np.zeros((programs.DENSE, programs.DENSE), np.float16)
+    for w in range(programs.DENSE):
+        for t in range(min(2, int(hdr[2]))):
+            row, val = int(planes[t, w, 0]), planes[t, w, 1:2].view(np.float32)[0]
+            if val != 0:
+                tile[row, w] = np.float16(val)
+    return tile
+
+
+def test_mapper_tile_from_term_planes_equals_dense_image(tok):
+    """The group cross kernel builds each edit's f16 mapper tile from the program's first two term
+    planes (tmax <= 2) instead of copying the dense image: for every program kind the two tiles are
+    bit-identical (Replace incl. a two-token word, Refine with -1 gathers, Reweight alone and chained
+    on both, a zero equalizer entry)."""
+    prompts = ["a painting of a squirrel eating a burger", "a painting of a lion eating a burger",
+               "a painting of a squirrel eating a big burger"]
+    rep = pc.AttentionReplace(prompts[:2], 10, 0.8, 0.4, tokenizer=tok, device=torch.device("cpu"))
+    ref = pc.AttentionRefine([prompts[0], prompts[2]], 10, 0.8, 0.4, tokenizer=tok, device=torch.device("cpu"))
+    m2 = torch.zeros(1, 77, 77)
+    m2[0, torch.arange(77), torch.arange(77)] = 1
+    m2[0, 3:5, 4] = 0.5                                # a target word fed by two source words (tmax 2)
+    eq = torch.rand(1, 77, generator=torch.Generator().manual_seed(3)).half().float()   # (dense: f16-exact)
+    eq[0, 5] = 0.0
+    progs = [rep._edit_program(), ref._edit_program(), programs.replace_program(m2),
+             programs.reweight_program(eq, 1, None), programs.reweight_program(eq, 1, rep._edit_program()),
+             programs.reweight_program(eq, 1, ref._edit_program())]
+    for prog in progs:
+        blob = prog.blob()
+        hdr = blob[:32].view(np.int32)
+        assert hdr[4] == 1 and hdr[2] <= 2
+        dense = blob[int(hdr[5]):].view(np.float16).reshape(prog.n_edits, programs.DENSE, programs.DENSE)
+        for e in range(prog.n_edits):
+            assert np.array_equal(_tile_from_terms(blob, e).view(np.uint16), dense[e].view(np.uint16))
