@@ -1569,7 +1569,8 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     // Q and its use would make the R_ONLY path wait for the tile and the own V before P0
     short8_t mreg[kMPer];
     {
-      const __amdgpu_buffer_rsrc_t rm = make_rsrc(mg, (int64_t)kMCh * 16);
+      // rows >= K are zero in the program: past the resource, so they read as zeros without a fetch
+      const __amdgpu_buffer_rsrc_t rm = make_rsrc(mg, (int64_t)K * P2P_PROGRAM_DENSE * 2);
 #pragma unroll
       for (int j = 0; j < kMPer; ++j)
         mreg[j] = __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rm, (tid + j * NT) * 16, 0, 0));
