@@ -1,5 +1,7 @@
 """One cross-attention configuration launched repeatedly (for rocprofv3 PMC passes):
 SD config-2 U-Net call, N = 8 (4 uncond + 4 cond), H = 8, K = 77, bf16 IO.
+The uncond group's K / V rows are equal and carry SHARED_KV, edit modes the R_ONLY hint (what the
+controllers pass inside cross_replace_steps).
 Usage: python tools/cross_one.py [iters] [mode: plain|edit|store|edit+store] [P] [d]"""
 import os
 import sys
@@ -23,11 +25,14 @@ def main(iters=20, mode="edit", P=4096, d=40):
     q = torch.randn(N, P, C, device="cuda", generator=g).to(torch.bfloat16)
     k = torch.randn(N, K, C, device="cuda", generator=g).to(torch.bfloat16)
     v = torch.randn(N, K, C, device="cuda", generator=g).to(torch.bfloat16)
+    # the uncond prompts "" share K / V (as in the pipeline): those rows equal, and SHARED_KV on that group
+    k[1:B] = k[0]
+    v[1:B] = v[0]
     o = torch.empty_like(q)
     store = torch.zeros(B * H, P, K, device="cuda") if "store" in mode else None
     slots = [-1] * B + [i * H for i in range(B)]
     # (edit modes carry the R_ONLY hint, as the controllers pass it inside cross_replace_steps)
-    grp = [(0, B, None, None), (B, B, prog if "edit" in mode else None, alpha if "edit" in mode else None, None,
+    grp = [(0, B, None, None, None, _hip.GROUP_F_SHARED_KV), (B, B, prog if "edit" in mode else None, alpha if "edit" in mode else None, None,
                                 _hip.GROUP_F_R_ONLY if "edit" in mode else 0)]
     for _ in range(iters):
         _hip.cross_attn(q, k, v, o, H, d ** -0.5, grp, store=store,
