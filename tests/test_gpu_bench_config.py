@@ -399,3 +399,59 @@ def test_config2_bf16unet_50_steps_teacher_forced(cuda, tok):
     print(f"configs[2] bf16 U-Net, 8 groups x {steps} steps, teacher-forced oracle: worst stored cross-map "
           f"|diff| {worst:.3e} = {worst / steps:.2e} per accumulated step")
     assert worst < 2e-3 * steps
+
+
+def test_bench_config_teacher_forced_every_call(cuda, tok):
+    """configs[1] exactly as benched -- bf16 U-Net, bf16 kernels, 1 source + 3 AttentionReplace edits
+    with the null_text LocalBlend, 50 DDIM steps -- with a TEACHER-FORCED oracle at EVERY attention
+    call: the call's own q / k / v (the product's bf16 projections) go through the oracle's fp32
+    softmax and reference controller (null_text.py:236-254: cross Replace with its time/word alpha,
+    self-injection inside self_replace_steps; AttentionStore main.py:129-142), and the product's
+    output must equal that edited attention times V within the bf16 bar (2^-7 max|V|) in all
+    50 x 32 calls, the stored cross maps within 2e-3 per accumulated step.  This pins the edit
+    itself at the benched precision, step by step, where the end-to-end edit-effect cosine (bar
+    0.70 here) only sees two diverging bf16 U-Net trajectories."""
+    steps = 50
+    prompts = pl.north_star_prompts()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    ctrl = pl.make_replace_controller(prompts, steps, device=cuda)
+    octrl = oracle_controller("replace", prompts, tok, steps, cuda)
+    orig = ctrl.attention
+    worst = {"self": 0.0, "cross": 0.0}
+    calls = {"self": 0, "cross": 0}
+
+    def split(t, heads):
+        t = t.float()
+        return t.reshape(t.shape[0], t.shape[1], heads, -1).permute(0, 2, 1, 3)     # [N, H, n, d]
+
+    def attention(q, k, v, heads, scale, is_cross, place_in_unet, mask=None):
+        out = orig(q, k, v, heads, scale, is_cross, place_in_unet, mask)
+        octrl.num_att_layers = ctrl.num_att_layers
+        N = q.shape[0]
+        attn = (torch.einsum("nhid,nhjd->nhij", split(q, heads), split(k, heads)) * scale).softmax(-1)
+        attn = octrl(attn.reshape(N * heads, q.shape[1], k.shape[1]), is_cross, place_in_unet)
+        ref = torch.einsum("nhij,nhjd->nhid", attn.reshape(N, heads, q.shape[1], k.shape[1]), split(v, heads))
+        ref = ref.permute(0, 2, 1, 3).reshape(q.shape)
+        kind = "cross" if is_cross else "self"
+        err = (out.float() - ref).abs().max().item() / v.float().abs().max().item()
+        worst[kind] = max(worst[kind], err)
+        calls[kind] += 1
+        return out
+
+    ctrl.attention = attention
+    with config.compute_mode("bf16"):
+        pl.run_edit_group(model, prompts, ctrl, pl.seed_latent(0), num_steps=steps)
+    torch.cuda.synchronize()
+    print(f"configs[1] as benched, teacher-forced at every call: {calls} calls, worst |O - O_oracle| / max|V| "
+          f"self {worst['self']:.2e}, cross {worst['cross']:.2e} (bar {2.0 ** -7:.2e})")
+    assert calls == {"self": 16 * steps, "cross": 16 * steps}, calls
+    assert worst["self"] < 2.0 ** -7 and worst["cross"] < 2.0 ** -7, worst
+    worst_map = 0.0
+    assert ctrl.cur_step == octrl.cur_step == steps
+    for key in ("down_cross", "mid_cross", "up_cross"):
+        ours, ref = ctrl.attention_store[key], octrl.attention_store[key]
+        assert len(ours) == len(ref) > 0, key
+        for x, y in zip(ours, ref):
+            worst_map = max(worst_map, (x - y).abs().max().item())
+    print(f"  stored cross maps: worst |diff| {worst_map:.3e} = {worst_map / steps:.2e} per accumulated step")
+    assert worst_map < 2e-3 * steps

@@ -42,10 +42,13 @@ def run(name, P, d, store):
     q = torch.randn(N, P, C, device="cuda").to(torch.bfloat16)
     k = torch.randn(N, K, C, device="cuda").to(torch.bfloat16)
     v = torch.randn(N, K, C, device="cuda").to(torch.bfloat16)
+    k[1:B] = k[0]      # the uncond prompts "" share K / V (SHARED_KV), as in the pipeline
+    v[1:B] = v[0]
     o = torch.empty_like(q)
     st = torch.zeros(B * H, P, K, device="cuda") if store else None
     slots = [-1] * B + [i * H for i in range(B)] if store else None
-    grp = [(0, B, None, None), (B, B, prog, alpha, None, _hip.GROUP_F_R_ONLY)]   # (alpha 1: the hint)
+    grp = [(0, B, None, None, None, int(os.environ.get("STAMPS_SHARED_KV", "1")) * _hip.GROUP_F_SHARED_KV),
+           (B, B, prog, alpha, None, _hip.GROUP_F_R_ONLY)]   # (alpha 1: the hint)
     fn = _hip.lib().p2p_diag_group_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     for _ in range(10):
