@@ -1057,8 +1057,7 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
 #define P2P_CROSS_STAMP(i)
 #endif
 
-// XV: experiments-only compile-time variant (0 = production)
-template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE, int XV = 0>
+template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>
 __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_attn_kernel(CrossArgs a) {
   using EK = typename MQ::elem;
   using EV = typename MP::elem;
@@ -1140,12 +1139,11 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
   // per instruction.  bf16 outputs with 16-byte rows instead go through LDS (the self kernels'
   // epilogue): after a workgroup barrier (every wave is done with K / V) each wave writes its 32
   // rows into the dead K / V image and stores them back as whole 16-byte row chunks, consecutive
-  // lanes along a row -- half the store instructions, whole lines.  (XV 202, experiments A/B: the
-  // direct store.)
+  // lanes along a row -- half the store instructions, whole lines.
   // Same-box rocprof (profiles/r05/ostore_ab/): d = 80 edit steps 16.43 -> 14.90 us, d = 160 17.44 ->
   // 16.56; the 8x8 layers (P = 64: half of every 128-query workgroup's rows past P) ran 2 % slower
   // and keep the direct store
-  const bool o16 = std::is_same<IO, uint16_t>::value && XV != 202 && a.P >= 256 && (a.ldo & 7) == 0 &&
+  const bool o16 = std::is_same<IO, uint16_t>::value && a.P >= 256 && (a.ldo & 7) == 0 &&
                    (a.bso & 7) == 0 && ((uintptr_t)a.o & 15) == 0;
   auto store_o = [&](const f32x16_t (&O)[NDT], float inv) __attribute__((always_inline)) {
     if constexpr (std::is_same<IO, uint16_t>::value) {
@@ -1542,8 +1540,7 @@ __global__ __launch_bounds__(64 * WAVES, (DENSE && D <= 80) ? 2 : 1) void cross_
     // the launch-wide prologue burst, not the latency, sets the first round trip.
     // d = 160 only: at d <= 80 (two workgroups per CU, 256 VGPRs) the tile and the own V held in
     // registers across P0 spill 56 VGPRs
-    // (XV 201, experiments A/B: the tile and the own V staged before the first barrier)
-    constexpr bool late = D > 80 && XV != 201;
+    constexpr bool late = D > 80;
     constexpr int kMCh = P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE / 8;   // 16-byte chunks of the tile
     constexpr int kMPer = (kMCh + NT - 1) / NT;
     const float* ce = reinterpret_cast<const float*>(prog + P2P_PROGRAM_HEADER_BYTES +
@@ -1970,17 +1967,6 @@ static hipError_t launch_cross_w(const CrossArgs& a, hipStream_t st) {
   const size_t tile = (size_t)P2P_PROGRAM_DENSE * P2P_PROGRAM_DENSE * sizeof(uint16_t);
   if (dense && dyn < tile) dyn = tile;
   dim3 grid(b.n_qtiles * a.H * a.N), block(64 * W);
-#ifdef P2P_EXPERIMENTS
-  if (dense && a.variant == 201 && D > 80) {
-    launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 201>), grid, block, dyn, st, b);
-    return hipGetLastError();
-  }
-  if (a.variant == 202) {
-    if (dense) launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense, 202>), grid, block, dyn, st, b);
-    else launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, false, 202>), grid, block, dyn, st, b);
-    return hipGetLastError();
-  }
-#endif
   if (dense)
     launch_kernel((cross_attn_kernel<IO, MQ, MP, D, W, kDense>), grid, block, dyn, st, b);
   else

@@ -48,8 +48,7 @@ constexpr int group_occupancy() {
   return (D <= 40 && !(EDIT && STORE)) || (D <= 80 && !EDIT && !STORE) ? 2 : 1;
 }
 
-// XV: experiments-only compile-time variant (0 = production)
-template <int D, int W, bool EDIT, bool STORE, int XV = 0>
+template <int D, int W, bool EDIT, bool STORE>
 __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) void cross_group_kernel(CrossArgs a) {
   constexpr bool kMaskCol = (D + 15) / 16 * 16 > D;   // K column D carries the key mask
   constexpr int DK = (D + 15) / 16 * 16;
@@ -77,8 +76,8 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
   // Plain groups only.  Same-box rocprof (profiles/r05/ostore_ab/group/): plain steps 17.23 -> 15.77
   // us, but edit steps 19.29 -> 19.53 (the 12 KiB of rows beside the mapper tile), so the edit
   // instantiations keep the direct row-per-lane store, as does plain + store (at two workgroups
-  // per CU the extra addressing spilled 6 VGPRs).  (XV 202, experiments A/B: the direct store.)
-  constexpr bool kLdsOut = XV != 202 && !EDIT && !STORE;
+  // per CU the extra addressing spilled 6 VGPRs).
+  constexpr bool kLdsOut = !EDIT && !STORE;
   constexpr int OS = D + 8;             // 16-byte aligned rows on distinct banks
   __shared__ __attribute__((aligned(16))) uint16_t Os[kLdsOut ? W * 32 * OS : 8];
 
@@ -639,15 +638,6 @@ hipError_t launch_group(const CrossArgs& a, hipStream_t st) {
   const bool store = a.any_store != 0;
   const size_t dyn = store ? (size_t)W * 32 * a.K * sizeof(float) : 0;
   dim3 grid(b.n_qtiles * a.H * a.n_groups), block(64 * W);
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 202) {
-    if (edit && store) launch_kernel((cross_group_kernel<D, W, true, true, 202>), grid, block, dyn, st, b);
-    else if (edit) launch_kernel((cross_group_kernel<D, W, true, false, 202>), grid, block, dyn, st, b);
-    else if (store) launch_kernel((cross_group_kernel<D, W, false, true, 202>), grid, block, dyn, st, b);
-    else launch_kernel((cross_group_kernel<D, W, false, false, 202>), grid, block, dyn, st, b);
-    return hipGetLastError();
-  }
-#endif
   if (edit && store) launch_kernel((cross_group_kernel<D, W, true, true>), grid, block, dyn, st, b);
   else if (edit) launch_kernel((cross_group_kernel<D, W, true, false>), grid, block, dyn, st, b);
   else if (store) launch_kernel((cross_group_kernel<D, W, false, true>), grid, block, dyn, st, b);
@@ -672,8 +662,7 @@ bool cross_group_eligible(const CrossArgs& a, int d) {
   if (a.edit_terms || a.K > P2P_MAX_KEYS_CROSS) return false;
   const int wgs = a.n_groups * a.H * ((a.P + 127) / 128);
 #ifdef P2P_EXPERIMENTS
-  if (a.variant == 120) return false;   // A/B: always the per-entry kernel
-  if (a.variant == 122 || a.variant == 123) return d == 40 || d == 80 || d == 160;   // A/B: always the group kernel (123: stamps)
+  if (a.variant == 123) return d == 40 || d == 80 || d == 160;   // clock stamps (tools/group_stamps.py)
 #endif
   return d == 40 && wgs >= 512;
 }

@@ -683,9 +683,6 @@ int run_self40(const SelfArgs& a, int d, hipStream_t st) {
   if (d == 80) {
     switch (a.variant) {
 #ifdef P2P_EXPERIMENTS
-      case 92: return (int)launch<80, 4, 2, 128, true, 1>(a, st);        // round 3's default
-      case 110: return (int)launch<80, 4, 2, 128, false, 1>(a, st);      // round 4's default
-      case 102: return (int)launch<80, 8, 1, 128, false, 1>(a, st);
       case 164: return (int)launch<80, 8, 1, 128, true, 1 | 128 | 256 | 512 | 16384 | 16>(a, st);  // default + stamps
 #endif
       // d = 80: 8 waves x ONE 32-row query block (two waves per SIMD), 128-key tiles, split staging

@@ -525,11 +525,7 @@ bool self_ring_eligible(const SelfArgs& a, int d) {
 
 int run_self_ring(const SelfArgs& a, int d, hipStream_t st) {
   (void)d;
-  bool halves = a.K <= 256;
-#ifdef P2P_EXPERIMENTS
-  if (a.variant == 200) halves = false;   // A/B: the 128-query ring kernel at every K
-#endif
-  if (halves) {
+  if (a.K <= 256) {
     SelfArgs b = a;
     b.n_qtiles = (a.P + 63) / 64;
     dim3 grid(b.n_qtiles * a.H * a.N), block(256);
