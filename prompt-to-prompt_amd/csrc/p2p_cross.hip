@@ -604,7 +604,9 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     } else if (more) {
       __syncthreads();   // every wave is done with this entry's K, V, mapper and coefficients
+      if (b == 1) P2P_GROUP_STAMP(22)
       write_entry(b + 1);
+      if (b == 1) P2P_GROUP_STAMP(23)
       __syncthreads();
       if constexpr (EDIT) {
         // the blend halves the next edit uses, from its coefficients (every wave scans the row

@@ -77,6 +77,10 @@ def run(name, P, d, store):
                          f"{np.median(ss[:, :, base + 2] - ss[:, :, base + 1]):.0f} pv+O "
                          f"{np.median(ss[:, :, base + 3] - ss[:, :, base + 2]):.0f} sync+next "
                          f"{np.median(ss[:, :, base + 4] - ss[:, :, base + 3]):.0f}")
+        if B > 2:   # entry 1's sync+next split: first barrier | write_entry (vmcnt(0) + LDS writes) | barrier + flags
+            parts.append(f"e1 sync+next = barrier {np.median(ss[:, :, 22] - ss[:, :, 10]):.0f} | wait + LDS writes "
+                         f"{np.median(ss[:, :, 23] - ss[:, :, 22]):.0f} | barrier + flags "
+                         f"{np.median(ss[:, :, 11] - ss[:, :, 23]):.0f}")
         total = np.median(ss[:, :, 2 + 5 * (B - 1) + 4] - t0)
         print(f"  {label} ({len(ss)} wg): total {total:.0f}\n    " + "\n    ".join(parts))
     starts = np.sort(s[:, 0, 0] - s[:, 0, 0].min())
