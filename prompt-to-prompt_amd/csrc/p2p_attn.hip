@@ -1054,7 +1054,7 @@ __device__ unsigned long long g_cross_stamps[4096 * 4 * 24];
   if (a.variant == 90 && logical < 4096 && wave < 4 && lane == 0)                                       \
     g_cross_stamps[(logical * 4 + wave) * 24 + (i)] = __builtin_amdgcn_s_memtime();
 #else
-#define P2P_CROSS_STAMP(i)
+#define P2P_CROSS_STAMP(i) do { } while (0);
 #endif
 
 template <typename IO, typename MQ, typename MP, int D, int WAVES, bool DENSE>

@@ -37,7 +37,7 @@ __device__ unsigned long long g_group_stamps[2048 * 4 * 24];
   if (a.variant == 123 && logical < 2048 && wave < 4 && lane == 0 && (i) < 24)                     \
     g_group_stamps[(logical * 4 + wave) * 24 + (i)] = __builtin_amdgcn_s_memtime();
 #else
-#define P2P_GROUP_STAMP(i)
+#define P2P_GROUP_STAMP(i) do { } while (0);
 #endif
 
 // two workgroups per CU (<= 256 VGPRs) where the state fits without spills: d = 40 unless it both
@@ -604,9 +604,13 @@ __global__ __launch_bounds__(64 * W, (group_occupancy<D, W, EDIT, STORE>())) voi
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     } else if (more) {
       __syncthreads();   // every wave is done with this entry's K, V, mapper and coefficients
-      if (b == 1) P2P_GROUP_STAMP(22)
+      if (b == 1) {
+        P2P_GROUP_STAMP(22)
+      }
       write_entry(b + 1);
-      if (b == 1) P2P_GROUP_STAMP(23)
+      if (b == 1) {
+        P2P_GROUP_STAMP(23)
+      }
       __syncthreads();
       if constexpr (EDIT) {
         // the blend halves the next edit uses, from its coefficients (every wave scans the row

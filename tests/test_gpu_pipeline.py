@@ -143,3 +143,28 @@ def test_cross_kv_cache_bit_identical(cuda):
           f"cache on vs off: equal {torch.equal(on, off1)} max |diff| {(on - off1).abs().max().item():.3e}")
     assert torch.equal(off1, off2), "the uncached pipeline is not run-to-run reproducible"
     assert torch.equal(on, off1)
+
+
+def test_edit_group_under_inference_mode(cuda):
+    """A controller built and run under torch.inference_mode() (its alpha table and the
+    loop's context then have no version counter): the per-step cross plan keys the alpha table by
+    its storage, the K / V projection cache stands aside, and the edit group is bit-identical to the
+    same group under torch.no_grad() (deterministic MIOpen, as in the K / V cache test)."""
+    prompts = pl.north_star_prompts()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    x_T = pl.seed_latent(9)
+    steps = 4
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        with config.compute_mode("bf16"):
+            with torch.no_grad():
+                want = pl.run_edit_group(model, prompts, pl.make_replace_controller(prompts, steps, device=cuda), x_T,
+                                         num_steps=steps)
+            with torch.inference_mode():
+                ctrl = pl.make_replace_controller(prompts, steps, device=cuda)
+                assert ctrl.cross_replace_alpha.is_inference()
+                got = pl.run_edit_group(model, prompts, ctrl, x_T, num_steps=steps)
+    finally:
+        torch.backends.cudnn.deterministic = det
+    assert torch.equal(got, want)
