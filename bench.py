@@ -466,6 +466,12 @@ def main():
     ap.add_argument("--seeds", type=int, default=0,
                     help="configs[3] sweep: time ALL of seeds 0..S-1, partitioned over the ranks and run\n"
                          "--groups-per-call at a time (--steps is then ignored); value = S / wall")
+    ap.add_argument("--eager", action="store_true",
+                    help="time the eager denoising loop for value (default: the DDIM steps replay HIP graphs\n"
+                         "captured after the first batch, pipeline.GraphedEditRunner; the per-launch kernel\n"
+                         "timing then comes from an eager pass of --instrumented batches right after)")
+    ap.add_argument("--instrumented", type=int, default=3,
+                    help="batches of the eager per-launch timing pass that follows a graphed timed region")
     ap.add_argument("--store-self", action="store_true",
                     help="also keep the 32x32/16x16/8x8 SELF maps (main.py AttentionStore default); the\n"
                          "north-star workload keeps only the maps AttentionStore/LocalBlend read")
@@ -509,25 +515,38 @@ def main():
     G = args.groups_per_call
 
     # one step = one batch of G groups: the runner the configs[3] GPU test drives through the same sweep
-    batch = pl.sweep_batch_runner(model, prompts, args.ddim_steps, store_self_maps=args.store_self, device=dev)
+    graphed = not args.eager
+    batch = pl.sweep_batch_runner(model, prompts, args.ddim_steps, store_self_maps=args.store_self, device=dev,
+                                  graphed=graphed)
+    # the same batches without graphs (the per-launch timing pass of a graphed run)
+    eager_batch = batch.eager_run if graphed else batch
 
-    # groups (seeds) partitioned across ranks round-robin: no collective on the data path
+    # groups (seeds) partitioned across ranks round-robin: no collective on the data path.  A
+    # graphed run always warms up once: its first batch is the eager run + the capture
+    n_warm = max(args.warmup, 1 if graphed else 0)
     if args.seeds > 0:
         all_seeds = list(range(args.seeds))
-        warm_seeds = [10 ** 6 + i for i in range(args.warmup * G)]
+        warm_seeds = [10 ** 6 + i for i in range(n_warm * G)]
     else:
         all_seeds = list(range(world * args.steps * G))
-        warm_seeds = [10 ** 6 + rank * args.warmup * G + i for i in range(args.warmup * G)]
-    for i in range(args.warmup):
+        warm_seeds = [10 ** 6 + rank * n_warm * G + i for i in range(n_warm * G)]
+    for i in range(n_warm):
         batch(warm_seeds[i * G:(i + 1) * G])
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     clock = ClockProbe(dev)
     timer.clock = clock
-    timer.enabled = True
-    t0 = time.perf_counter()
 
+    def max_over_ranks(x):
+        if distributed:
+            tt = torch.tensor([x], device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            return tt.item()
+        return x
+
+    timer.enabled = not graphed   # graph replays make no per-launch calls: the eager pass below times them
+    t0 = time.perf_counter()
     clock.sample("start")
     timer.end_batch()     # (batch 0's start mark)
 
@@ -545,13 +564,36 @@ def main():
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     timer.enabled = False
-    if distributed:
-        tt = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
     n_total = len(all_seeds)
+
+    eager_line = None
+    mine = sweep.batches(all_seeds, rank, world, G)
+    inst = mine[:args.instrumented] if graphed else mine
+    if graphed:
+        # the per-launch timing pass: the same batches (this rank's first --instrumented), eager,
+        # every hot-path launch bracketed by the kernels' own HIP events, the clock probed under
+        # G1/G7; its wall time is reported beside value as eager_value
+        timer.enabled = True
+        t1 = time.perf_counter()
+        clock.sample("start")
+        timer.end_batch()
+        for i, b in enumerate(inst):
+            eager_batch(b)
+            timer.end_batch()
+        clock.sample("end")
+        torch.cuda.synchronize(dev)
+        if distributed:
+            dist.barrier()
+        elapsed_inst = max_over_ranks(time.perf_counter() - t1)
+        timer.enabled = False
+        n_inst = sum(len(b) for b in inst)
+        if distributed:
+            tn = torch.tensor([float(n_inst)], device=dev)
+            dist.all_reduce(tn)
+            n_inst = int(tn.item())
+        eager_line = {"value": n_inst / elapsed_inst, "groups": n_inst, "seconds": elapsed_inst}
     assert lat_all.shape == (n_total, B, 4, 64, 64) and maps_all.shape == (n_total, B, 16, 16, 77)
     assert torch.isfinite(lat_all).all() and torch.isfinite(maps_all).all()
     # each source prompt's gathered map row is an average of probability rows: it sums to 1
@@ -564,7 +606,7 @@ def main():
     for i, ms_b, dom in timer.per_batch():
         print(f"[bench rank {rank}] batch {i} gpu {ms_b:.1f} ms  dominant avg "
               f"{dom * 1e3 if dom else float('nan'):.1f} us", file=sys.stderr, flush=True)
-    unet_calls = len(sweep.batches(all_seeds, rank, world, G)) * args.ddim_steps   # this rank's U-Net calls
+    unet_calls = len(inst) * args.ddim_steps   # this rank's U-Net calls in the per-launch timing pass
     attn_total = timer.attn_total(peak, unet_calls)
     if rank == 0:
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms else None
@@ -603,6 +645,12 @@ def main():
                        "groups_per_call": G, "groups_total": n_total, "unet_dtype": args.unet_dtype,
                        "self_maps_kept": args.store_self, "gathered": "final latents + 16x16 cross maps (1 all-gather)",
                        "parallelism": f"replicas x{world} (groups by seed)"},
+            "loop": ("HIP graphs: the 50 DDIM steps of each batch replay graphs captured once per batch size "
+                     "(pipeline.GraphedEditRunner; bit-identical to the eager loop, tests/test_gpu_pipeline.py)"
+                     if graphed else "eager"),
+            # graphed runs: the eager loop's throughput over the per-launch timing pass that follows
+            # (the same batches' first --instrumented of this rank; every roofline field comes from it)
+            "eager_value": eager_line,
             "roofline": roofline, "cpu_baseline": cpu,
             # every attention launch of the timed run together (north star: ">= 45 % of bf16 MFMA peak
             # in the attention kernels"), HIP-event timed, with the per-geometry split

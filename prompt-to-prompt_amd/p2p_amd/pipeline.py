@@ -9,6 +9,7 @@ random-init SD-shaped U-Net and the DDIM scheduler of null_text.py:16-20.
 """
 from __future__ import annotations
 
+import time
 from typing import List, Optional, Sequence
 
 import torch
@@ -138,13 +139,14 @@ def run_edit_groups(model: SyntheticStableDiffusion, prompt_groups: Sequence[Seq
 
 
 def sweep_batch_runner(model: SyntheticStableDiffusion, prompts: Sequence[str], num_steps: int = 50,
-                       store_self_maps: bool = False, device=None):
+                       store_self_maps: bool = False, device=None, graphed: bool = False):
     """The unit of work bench.py times and the configs[3] sweep runs (sweep.run_batched_sweep):
     run(seeds) denoises len(seeds) edit groups -- each 1 source + 3 AttentionReplace edits with
     LocalBlend and its own seed -- one U-Net call per DDIM step (controllers.GroupBatch when
     len(seeds) > 1), and returns the final latents [g, B, 4, 64, 64] and each group's reduced
     stored maps [g, B, 16, 16, 77] (aggregate_attention's 16x16 cross average per prompt,
-    main.py:293-307)."""
+    main.py:293-307).  ``graphed``: the DDIM steps replay HIP graphs captured after the first
+    batch of each size (GraphedEditRunner) -- the same launches, without the per-kernel gaps."""
     from . import controllers
     B = len(prompts)
 
@@ -163,7 +165,129 @@ def sweep_batch_runner(model: SyntheticStableDiffusion, prompts: Sequence[str], 
         return lat.reshape(len(seeds), B, *lat.shape[1:]), maps
 
     run.out_shapes = [(B, 4, 64, 64), (B, 16, 16, 77)]
-    return run
+    if not graphed:
+        return run
+    return GraphedEditRunner(model, prompts, num_steps, make_ctrl, run)
+
+
+class GraphedEditRunner:
+    """sweep_batch_runner's run(seeds) with every DDIM step replayed from a HIP graph.
+
+    The first batch of each size runs eagerly on the runner's capture stream (it returns real
+    results, and it makes every first-use library search -- MIOpen's convolution find, hipBLASLt's
+    heuristics -- and every host table of the controllers happen outside a capture).  Then fresh
+    controllers for that batch size are built and the 50 steps of ptp_utils.diffusion_step are
+    captured, one graph per step, into one memory pool: each step's host plan (the controller's
+    counters, cross_replace_alpha row, R_ONLY hint, self-injection window, store add / overwrite,
+    LocalBlend start) is decided while capturing, exactly as the eager loop decides it at that step,
+    and baked into that step's launches.  A later batch refills the static inputs -- x_T and the
+    re-encoded text context -- and replays the 50 graphs in order; the captured controllers' running
+    sums then hold that batch's maps (they are overwritten at step 0 as in an eager run), and their
+    host state (cur_step = 50) is the state an eager run ends in, so reduce_maps reads them as usual.
+
+    Not captured: the text encoder (runs eagerly per batch, its output copied into the static
+    context).  The cross K / V projections are captured in step 0's graph and read by the later
+    steps' (ptp_utils._cross_kv's capture rules), so every replayed batch projects its own context
+    once, as an eager group does."""
+
+    def __init__(self, model, prompts, num_steps, make_ctrl, eager_run, guidance_scale=7.5):
+        self.model, self.prompts, self.num_steps = model, list(prompts), num_steps
+        self.make_ctrl, self.eager_run, self.guidance_scale = make_ctrl, eager_run, guidance_scale
+        self.out_shapes = eager_run.out_shapes
+        self.B = len(prompts)
+        self.stream = None
+        self.plans = {}
+
+    def __call__(self, seeds):
+        seeds = list(seeds)
+        plan = self.plans.get(len(seeds))
+        if plan is None:
+            return self._first(seeds)
+        return self._replay(plan, seeds)
+
+    # ------------------------------------------------------------------ first batch of a size
+    def _first(self, seeds):
+        dev = self.model.device
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        self.stream.wait_stream(cur)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(self.stream):
+            out = tuple(r.clone() for r in self.eager_run(seeds))
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            self.plans[len(seeds)] = self._capture(len(seeds))
+        torch.cuda.synchronize(dev)
+        self.first_seconds = (t1 - t0, time.perf_counter() - t1)   # (eager batch, capture)
+        return out
+
+    def _context(self, G):
+        from . import ptp_utils
+        prompts = self.prompts * G
+        text = ptp_utils._encode(self.model, prompts, self.model.text_encoder)
+        uncond = ptp_utils._encode(self.model, [""] * len(prompts), self.model.text_encoder)
+        return ptp_utils.unet_context(self.model, torch.cat([uncond, text]))
+
+    @torch.no_grad()
+    def _capture(self, G):
+        from . import controllers
+        from . import ptp_utils as pu
+        model, dev, B = self.model, self.model.device, self.B
+        members = [self.make_ctrl() for _ in range(G)]
+        ctrl = members[0] if G == 1 else controllers.GroupBatch(members)
+        for m in members:
+            _prime_for_capture(m, dev)
+        pu.register_attention_control(model, ctrl)
+        ctx = self._context(G).clone()
+        x = torch.zeros(G * B, 4, 64, 64, device=dev)
+        model.scheduler.set_timesteps(self.num_steps)
+        ts = list(model.scheduler.timesteps)
+        t_dev = [torch.full((1,), int(t), dtype=torch.int64, device=dev) for t in ts]
+        pool = torch.cuda.graph_pool_handle()
+        graphs = []
+        lat = x
+        torch.cuda.synchronize(dev)
+        for t, td in zip(ts, t_dev):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, stream=self.stream):
+                lat = pu.diffusion_step(model, ctrl, lat, ctx, t, self.guidance_scale, t_unet=td)
+            graphs.append(g)
+        # the captured K / V cache entries: their tensors are written by step 0's graph and read by
+        # the others, so they live as long as the graphs (an eager call replaces the module's entry)
+        kv = [mod.__dict__["_p2p_kv"] for mod in model.unet.modules()
+              if "_p2p_kv" in mod.__dict__ and mod.__dict__["_p2p_kv"][5] and mod.__dict__["_p2p_kv"][0]() is ctx]
+        return {"graphs": graphs, "x": x, "ctx": ctx, "out": lat, "ctrl": ctrl, "members": members,
+                "t_dev": t_dev, "pool": pool, "kv": kv}
+
+    # ------------------------------------------------------------------ later batches
+    @torch.no_grad()
+    def _replay(self, plan, seeds):
+        from . import controllers
+        G, B = len(seeds), self.B
+        x_T = torch.cat([seed_latent(s).expand(B, 4, 64, 64) for s in seeds])
+        plan["x"].copy_(x_T)
+        plan["ctx"].copy_(self._context(G))
+        for g in plan["graphs"]:
+            g.replay()
+        lat = plan["out"].clone().reshape(G, B, 4, 64, 64)
+        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in plan["members"]])
+        return lat, maps
+
+
+def _prime_for_capture(ctrl, device):
+    """Make an edit controller's first call free of host <-> device copies (which a capture cannot
+    hold): its device edit program and the host copy of cross_replace_alpha are built now."""
+    from . import controllers
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:   # the key the kernels' tensors give (cuda:N)
+        device = torch.device("cuda", torch.cuda.current_device())
+    if isinstance(ctrl, controllers.AttentionControlEdit):
+        try:
+            ctrl._device_program(device)
+        except controllers.NotFusable:
+            return
+        ctrl._cross_step(device, ctrl.cross_replace_alpha.shape[-1])
 
 
 # BASELINE.json configs[2]: AttentionRefine + AttentionReweight (equalizer) groups whose 16/32-res

@@ -21,16 +21,19 @@ from .ptp_words import get_time_words_attention_alpha, get_word_inds, update_alp
 
 
 # ------------------------------------------------------------------ sampling loop
-def diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource=False):
+def diffusion_step(model, controller, latents, context, t, guidance_scale, low_resource=False, t_unet=None):
     """One CFG denoising step (ptp_utils.py:65-76).  With this library's DDIM scheduler and a
     controller whose step_callback is its own, the CFG combine, the DDIM step and LocalBlend's
-    latent blend run as one HIP kernel (p2p_latent_step) -- same result, bit for bit."""
+    latent blend run as one HIP kernel (p2p_latent_step) -- same result, bit for bit.
+    ``t_unet``: the same timestep as a device tensor for the U-Net (a captured step must not copy
+    a host timestep to the device); the scheduler keeps reading the host ``t``."""
+    tu = t if t_unet is None else t_unet
     if low_resource:
-        eps_u = model.unet(latents, t, encoder_hidden_states=context[0])["sample"]
-        eps_c = model.unet(latents, t, encoder_hidden_states=context[1])["sample"]
+        eps_u = model.unet(latents, tu, encoder_hidden_states=context[0])["sample"]
+        eps_c = model.unet(latents, tu, encoder_hidden_states=context[1])["sample"]
         eps = None
     else:
-        eps = model.unet(torch.cat([latents] * 2), t, encoder_hidden_states=context)["sample"]
+        eps = model.unet(torch.cat([latents] * 2), tu, encoder_hidden_states=context)["sample"]
         eps_u, eps_c = eps.chunk(2)
     fused = _fused_latent_step(model, controller, eps, eps_u, eps_c, latents, t, guidance_scale)
     if fused is not None:
@@ -217,19 +220,31 @@ def _cross_kv(module, context, w):
     context by identity (a weak reference: a new tensor, even at a recycled address, misses) and
     its version counter (an in-place change misses), and the stacked weight object (rebuilt by
     _stacked_weight whenever a projection weight changes).  Not cached: inference-mode tensors (no
-    version counter) and calls under stream capture (a graph replays its own GEMM on refilled
-    static inputs, e.g. null-text's per-step uncond embeddings)."""
+    version counter).
+    Under stream capture an entry is made and hit only among captures: the first captured call
+    records its GEMM in its graph (which recomputes K / V from the static context a replay has
+    refilled, e.g. pipeline.GraphedEditRunner's step 0 or null-text's per-step uncond embeddings)
+    and the later captured steps read that GEMM's output; an entry made eagerly is never hit by a
+    capture (its K / V are of the context's content at that time, not at replay), and a captured
+    entry never by an eager call (its K / V exist only once a replay ran).  The SHARED_KV row
+    classes need a device read, so captured entries carry none."""
     import weakref
-    if (not CACHE_CROSS_KV or context.is_inference() or context.requires_grad
-            or (context.is_cuda and torch.cuda.is_current_stream_capturing())):
+    if not CACHE_CROSS_KV or context.is_inference() or context.requires_grad:
         return torch.nn.functional.linear(context, w), None
+    capturing = _capturing(context)
     hit = module.__dict__.get("_p2p_kv")
-    if hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w:
+    if (hit is not None and hit[0]() is context and hit[1] == context._version and hit[2] is w
+            and hit[5] == capturing):
         return hit[3], hit[4]
     kv = torch.nn.functional.linear(context, w)
-    rows = kv_row_classes(kv)
-    module.__dict__["_p2p_kv"] = (weakref.ref(context), context._version, w, kv, rows)
+    rows = None if capturing else kv_row_classes(kv)
+    module.__dict__["_p2p_kv"] = (weakref.ref(context), context._version, w, kv, rows, capturing)
     return kv, rows
+
+
+def _capturing(t) -> bool:
+    """True while ``t``'s device stream is being captured into a HIP graph."""
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
 
 
 def kv_row_classes(kv):

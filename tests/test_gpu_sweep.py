@@ -90,3 +90,6 @@ def test_bench_under_torchrun_world1_rccl(cuda):
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     print("torchrun world-1 bench:", line["value"], "edit-groups/s at 2 DDIM steps", flush=True)
     assert line["n_gpus"] == 1 and line["config"]["groups_total"] == 2 and line["value"] > 0
+    # the default loop replays HIP graphs; the per-launch timing pass that follows ran eagerly
+    assert line["loop"].startswith("HIP graphs") and line["eager_value"]["groups"] == 2
+    assert line["roofline"]["launches"] > 0

@@ -296,6 +296,45 @@ def test_cross_kv_cache_rules():
         pu.CACHE_CROSS_KV = True
 
 
+def test_cross_kv_cache_capture_rules():
+    """Under stream capture (ptp_utils._capturing, simulated here) the K / V cache keeps eager and
+    captured entries apart: a capture never hits an eagerly made entry (its K / V are of the
+    context's content before the replay refills it) and makes its own (the first captured step
+    records the GEMM, the later captured steps reuse its output, without SHARED_KV row classes);
+    an eager call never hits a captured entry (its K / V exist only after a replay)."""
+    from p2p_amd import ptp_utils as pu
+
+    class M:
+        pass
+    m = M()
+    g = torch.Generator().manual_seed(1)
+    w = torch.randn(16, 8, generator=g)
+    ctx = torch.randn(2, 5, 8, generator=g)
+    calls = []
+    orig, orig_cap = torch.nn.functional.linear, pu._capturing
+    state = {"capturing": False}
+
+    def counting(x, weight, bias=None):
+        calls.append(state["capturing"])
+        return orig(x, weight, bias)
+    torch.nn.functional.linear = counting
+    pu._capturing = lambda t: state["capturing"]
+    try:
+        eager, rows = pu._cross_kv(m, ctx, w)           # eager entry (warm-up before a capture)
+        assert rows == (0, 1) and calls == [False]
+        state["capturing"] = True
+        cap, crow = pu._cross_kv(m, ctx, w)             # capture: misses the eager entry
+        assert calls == [False, True] and crow is None and cap is not eager
+        cap2, _ = pu._cross_kv(m, ctx, w)               # a later captured step: hits the captured entry
+        assert cap2 is cap and len(calls) == 2
+        state["capturing"] = False
+        again, rows2 = pu._cross_kv(m, ctx, w)          # eager: never the captured entry
+        assert again is not cap and len(calls) == 3 and rows2 == (0, 1)
+    finally:
+        torch.nn.functional.linear = orig
+        pu._capturing = orig_cap
+
+
 def test_kv_row_classes_and_shared_kv_hint():
     """ptp_utils.kv_row_classes marks runs of bit-identical K / V rows (the uncond prompts "" of a
     group); _hip.shared_kv_hint turns a group whose rows all share one class into SHARED_KV."""
