@@ -5,7 +5,10 @@ One "step" = one complete edit group of BASELINE.json configs[1]: SD-v1.4-shaped
 (random init), 512x512 (64x64 latent), 1 source + 3 AttentionReplace edits with
 null_text-form LocalBlend, CFG 7.5 (U-Net batch 8), 50 DDIM steps, cross_replace 0.8,
 self_replace 0.4 -- every attention call is one fused HIP kernel (edits + store in it).
-Text encoding is replaced by a synthetic context, no VAE decode.
+Text encoding is replaced by a synthetic context, no VAE decode.  By default each batch's 50
+DDIM steps replay HIP graphs captured once (pipeline.GraphedEditRunner, during the warm-up);
+the per-launch kernel timing (roofline, clock, attention totals) comes from an eager pass of the
+same batches right after the timed region (--eager: time the eager loop itself).
 
 Multi-GPU: one process per GPU (torchrun); edit groups (seeds) are partitioned across ranks
 (weak scaling, no data-path collective); the final latents are all-gathered over RCCL once
@@ -593,7 +596,9 @@ def main():
             tn = torch.tensor([float(n_inst)], device=dev)
             dist.all_reduce(tn)
             n_inst = int(tn.item())
-        eager_line = {"value": n_inst / elapsed_inst, "groups": n_inst, "seconds": elapsed_inst}
+        eager_line = {"value": n_inst / elapsed_inst, "groups": n_inst, "seconds": elapsed_inst,
+                      "loop": "eager, every hot-path launch bracketed by its kernels' HIP events and the "
+                              "clock probed beside every 25th G1/G7 launch"}
     assert lat_all.shape == (n_total, B, 4, 64, 64) and maps_all.shape == (n_total, B, 16, 16, 77)
     assert torch.isfinite(lat_all).all() and torch.isfinite(maps_all).all()
     # each source prompt's gathered map row is an average of probability rows: it sums to 1
