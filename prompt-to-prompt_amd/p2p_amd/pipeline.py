@@ -185,6 +185,10 @@ class GraphedEditRunner:
     sums then hold that batch's maps (they are overwritten at step 0 as in an eager run), and their
     host state (cur_step = 50) is the state an eager run ends in, so reduce_maps reads them as usual.
 
+    The graphs read the model's weights (and the stacked projection weights built from them) where
+    they were at capture: after changing any weight, call release() -- the next batch of each size
+    then runs eagerly and captures again.
+
     Not captured: the text encoder (runs eagerly per batch, its output copied into the static
     context).  The cross K / V projections are captured in step 0's graph and read by the later
     steps' (ptp_utils._cross_kv's capture rules), so every replayed batch projects its own context
@@ -196,6 +200,10 @@ class GraphedEditRunner:
         self.out_shapes = eager_run.out_shapes
         self.B = len(prompts)
         self.stream = None
+        self.plans = {}
+
+    def release(self):
+        """Drop every captured plan (graphs, memory pool, controllers)."""
         self.plans = {}
 
     def __call__(self, seeds):
@@ -219,6 +227,8 @@ class GraphedEditRunner:
             t1 = time.perf_counter()
             self.plans[len(seeds)] = self._capture(len(seeds))
         torch.cuda.synchronize(dev)
+        for r in out:            # made on the capture stream, read on the caller's
+            r.record_stream(cur)
         self.first_seconds = (t1 - t0, time.perf_counter() - t1)   # (eager batch, capture)
         return out
 
@@ -250,7 +260,9 @@ class GraphedEditRunner:
         torch.cuda.synchronize(dev)
         for t, td in zip(ts, t_dev):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, stream=self.stream):
+            # thread-local capture: another thread's HIP calls (an RCCL proxy thread of a
+            # multi-GPU run) do not invalidate this thread's capture
+            with torch.cuda.graph(g, pool=pool, stream=self.stream, capture_error_mode="thread_local"):
                 lat = pu.diffusion_step(model, ctrl, lat, ctx, t, self.guidance_scale, t_unet=td)
             graphs.append(g)
         # the captured K / V cache entries: their tensors are written by step 0's graph and read by
