@@ -55,7 +55,9 @@ for step in "$@"; do
       grep '^{' "$out/prof.log" | tail -1 | tee "$out/bench_under_rocprof.json"
       find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;
       db=$(find "$out/prof" -name "*.db" | head -1)
-      if [ -n "$db" ]; then python3 tools/rocpd_summary.py "$db" > "$out/rocprof_summary.txt"; sed -n '/hot path/,$p' "$out/rocprof_summary.txt" | head -14; fi
+      # (--split-last: the G1/G7 launches of bench.py's eager timing pass -- 3 batches x 250 by default
+      # -- against the warm-up and graph replays before it)
+      if [ -n "$db" ]; then python3 tools/rocpd_summary.py "$db" --split-last "${P2P_SPLIT_LAST:-750}" > "$out/rocprof_summary.txt"; sed -n '/hot path/,$p' "$out/rocprof_summary.txt" | head -14; tail -4 "$out/rocprof_summary.txt"; fi
       rm -rf "$out/prof" ;;   # (the trace database of a 20-group run is far past gpurun's 64 MiB return cap)
     pmc)
       name=${arg%%:*}; counters=${arg#*:}
