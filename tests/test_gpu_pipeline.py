@@ -178,7 +178,8 @@ def test_graphed_runner_bit_identical(cuda):
     after the capture, a batch of new seeds equals the eager runner's, and a replay of the first
     batch's seeds equals that first (eager) batch -- final latents and reduced 16x16 cross maps,
     bit for bit (the captured controllers' running sums, blend sums and LocalBlend plan start fresh
-    at every replay).  The bench's 50 steps: the self-injection window (20), the cross-replace
+    at every replay).  Then release() and a fresh capture, and a runner that keeps every self map
+    too (bench.py --store-self), whose averaged self maps equal an eager group's.  The bench's 50 steps: the self-injection window (20), the cross-replace
     window (40) and LocalBlend from step 11 all change inside the run.  Reproducible convolutions,
     as the K / V cache test."""
     prompts = pl.north_star_prompts()
@@ -202,5 +203,24 @@ def test_graphed_runner_bit_identical(cuda):
                     for w, g_ in zip(want, got):
                         assert w.shape == g_.shape
                         assert torch.equal(w, g_), (G, (w - g_).abs().max().item())
+            # release(): the next batch runs eagerly and captures again, with the same results
+            graphed.release()
+            assert not graphed.plans
+            again = graphed([300])
+            assert 1 in graphed.plans
+            for w, g_ in zip(eager([300]), again):
+                assert torch.equal(w, g_)
+            # the kept self maps (bench.py --store-self): every 32x32 / 16x16 / 8x8 self map stored too
+            eager_s = pl.sweep_batch_runner(model, prompts, steps, device=cuda, store_self_maps=True)
+            graphed_s = pl.sweep_batch_runner(model, prompts, steps, device=cuda, store_self_maps=True, graphed=True)
+            graphed_s([400])
+            ctrl = graphed_s.plans[1]["ctrl"]
+            assert ctrl.store_self_maps and len(ctrl.attention_store["up_self"]) == 6
+            for w, g_ in zip(eager_s([401]), graphed_s([401])):
+                assert torch.equal(w, g_)
+            want_self = ctrl.get_average_attention()["down_self"][0].clone()
+            eager_ctrl = pl.make_replace_controller(prompts, steps, device=cuda, store_self_maps=True)
+            pl.run_edit_group(model, prompts, eager_ctrl, pl.seed_latent(401), num_steps=steps)
+            assert torch.equal(eager_ctrl.get_average_attention()["down_self"][0], want_self)
     finally:
         torch.backends.cudnn.enabled = det
