@@ -147,31 +147,40 @@ def sweep_batch_runner(model: SyntheticStableDiffusion, prompts: Sequence[str], 
     stored maps [g, B, 16, 16, 77] (aggregate_attention's 16x16 cross average per prompt,
     main.py:293-307).  ``graphed``: the DDIM steps replay HIP graphs captured after the first
     batch of each size (GraphedEditRunner) -- the same launches, without the per-kernel gaps."""
-    from . import controllers
-    B = len(prompts)
-
     def make_ctrl():
         return make_replace_controller(prompts, num_steps, device=device, store_self_maps=store_self_maps)
+    return edit_batch_runner(model, prompts, make_ctrl, num_steps, graphed=graphed)
+
+
+def edit_batch_runner(model: SyntheticStableDiffusion, prompts: Sequence[str], make_ctrl, num_steps: int = 50,
+                      graphed: bool = False, map_res: int = 16):
+    """run(seeds) for any edit controller: ``make_ctrl()`` builds one group's controller (an
+    AttentionStore subclass: its maps are reduced at ``map_res``); len(seeds) groups of ``prompts``
+    share each U-Net call (controllers.GroupBatch when more than one).  Returns the final latents
+    [g, B, 4, 64, 64] and the reduced cross maps [g, B, map_res, map_res, 77].  ``graphed``: a
+    GraphedEditRunner around the same run."""
+    from . import controllers
+    B = len(prompts)
 
     def run(seeds):
         if len(seeds) == 1:
             ctrl = make_ctrl()
             lat = run_edit_group(model, prompts, ctrl, seed_latent(seeds[0]), num_steps=num_steps)
-            return lat[None], controllers.reduce_maps(ctrl, 16, ["up", "down"], True, B)[None]
+            return lat[None], controllers.reduce_maps(ctrl, map_res, ["up", "down"], True, B)[None]
         members = [make_ctrl() for _ in seeds]
         lat = run_edit_groups(model, [prompts] * len(seeds), controllers.GroupBatch(members),
                               [seed_latent(s) for s in seeds], num_steps=num_steps)
-        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in members])
+        maps = torch.stack([controllers.reduce_maps(m, map_res, ["up", "down"], True, B) for m in members])
         return lat.reshape(len(seeds), B, *lat.shape[1:]), maps
 
-    run.out_shapes = [(B, 4, 64, 64), (B, 16, 16, 77)]
+    run.out_shapes = [(B, 4, 64, 64), (B, map_res, map_res, 77)]
     if not graphed:
         return run
-    return GraphedEditRunner(model, prompts, num_steps, make_ctrl, run)
+    return GraphedEditRunner(model, prompts, num_steps, make_ctrl, run, map_res=map_res)
 
 
 class GraphedEditRunner:
-    """sweep_batch_runner's run(seeds) with every DDIM step replayed from a HIP graph.
+    """edit_batch_runner's run(seeds) with every DDIM step replayed from a HIP graph.
 
     The first batch of each size runs eagerly on the runner's capture stream (it returns real
     results, and it makes every first-use library search -- MIOpen's convolution find, hipBLASLt's
@@ -194,7 +203,8 @@ class GraphedEditRunner:
     steps' (ptp_utils._cross_kv's capture rules), so every replayed batch projects its own context
     once, as an eager group does."""
 
-    def __init__(self, model, prompts, num_steps, make_ctrl, eager_run, guidance_scale=7.5):
+    def __init__(self, model, prompts, num_steps, make_ctrl, eager_run, guidance_scale=7.5, map_res=16):
+        self.map_res = map_res
         self.model, self.prompts, self.num_steps = model, list(prompts), num_steps
         self.make_ctrl, self.eager_run, self.guidance_scale = make_ctrl, eager_run, guidance_scale
         self.out_shapes = eager_run.out_shapes
@@ -283,7 +293,8 @@ class GraphedEditRunner:
         for g in plan["graphs"]:
             g.replay()
         lat = plan["out"].clone().reshape(G, B, 4, 64, 64)
-        maps = torch.stack([controllers.reduce_maps(m, 16, ["up", "down"], True, B) for m in plan["members"]])
+        maps = torch.stack([controllers.reduce_maps(m, self.map_res, ["up", "down"], True, B)
+                            for m in plan["members"]])
         return lat, maps
 
 

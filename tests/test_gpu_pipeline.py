@@ -224,3 +224,30 @@ def test_graphed_runner_bit_identical(cuda):
             assert torch.equal(eager_ctrl.get_average_attention()["down_self"][0], want_self)
     finally:
         torch.backends.cudnn.enabled = det
+
+
+def test_graphed_runner_refine_reweight_groups(cuda):
+    """configs[2]'s controllers through the graphed loop: two prompt groups per U-Net call, each an
+    AttentionReweight (equalizer) chained on an AttentionRefine whose 16/32-res cross maps are all
+    kept (pipeline.make_refine_reweight_controller), 50 steps -- the final latents and reduced 16x16
+    maps bit-identical to the eager runner (reproducible convolutions, as above)."""
+    prompts = [pl.REFINE_SOURCE] + pl.REFINE_EDITS
+    tok = controllers.get_tokenizer()
+    model = pl.SyntheticStableDiffusion(device=cuda, dtype=torch.bfloat16)
+    steps = 50
+
+    def make_ctrl():
+        return pl.make_refine_reweight_controller(prompts, steps, device=cuda, tokenizer=tok)
+    det = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        with config.compute_mode("bf16"):
+            eager = pl.edit_batch_runner(model, prompts, make_ctrl, steps)
+            graphed = pl.edit_batch_runner(model, prompts, make_ctrl, steps, graphed=True)
+            graphed([500, 501])                       # eager + capture
+            ctrl = graphed.plans[2]["ctrl"]
+            assert isinstance(ctrl, controllers.GroupBatch) and len(ctrl.members) == 2
+            for w, g_ in zip(eager([502, 503]), graphed([502, 503])):
+                assert torch.equal(w, g_), (w - g_).abs().max().item()
+    finally:
+        torch.backends.cudnn.enabled = det
